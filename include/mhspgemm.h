@@ -1,0 +1,133 @@
+/*
+ * mhspgemm.h -- C-ABI of the MI355X-native hash-accumulator SpGEMM.
+ *
+ * Drop-in boundary for the reference's call path (yyssys/MH-SpGEMM):
+ *   void MH_spgemm(const CSR &A, CSR &B, CSR &C, Timing &Timing, Tool &tools)
+ *     (/root/reference/src/main.cu:12-72)
+ * which the reference's main() calls on device-resident A and B
+ * (src/main.cu:110-124) and which leaves C (C.d_ptr/d_col/d_val, C.nnz)
+ * on the device.  Every entry point below is extern "C", takes plain
+ * pointers and sizes, and never throws; failures return an mhs_status and
+ * leave a message in mhs_last_error().
+ *
+ * Data contract (same as the reference):
+ *   - CSR, zero-based, int32 row_ptr[M+1] / col_idx[nnz], double val[nnz].
+ *   - A is M x K, B is K x N (the reference computes A*A: B = A, main.cu:101).
+ *   - B's column indices are sorted ascending within each row (the reference
+ *     relies on it in Form_mask_matrix_B.cuh:442-447 and guarantees it in
+ *     mmio_read.h:150).  Violations are detected and reported as
+ *     MHS_ERR_INVALID rather than producing a wrong C.
+ *   - C's pattern is structural (cancellation zeros are kept), columns are
+ *     sorted ascending per row, duplicates in A or B are summed.
+ *   - Values are FP64; summation order on the GPU is not fixed, so values
+ *     match a sequential reference to rounding (the north-star bound is
+ *     1e-6 relative), row_ptr and col_idx match bit-exactly.
+ */
+#ifndef MHSPGEMM_H
+#define MHSPGEMM_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MHS_ABI_VERSION 1
+
+typedef enum mhs_status {
+    MHS_OK = 0,
+    MHS_ERR_HIP = 1,      /* a HIP runtime call failed (reference: CHECK_ERROR throw, common.h:85-95) */
+    MHS_ERR_OOM = 2,      /* device allocation failed */
+    MHS_ERR_INVALID = 3,  /* bad argument, dimension mismatch, unsorted or out-of-range columns */
+    MHS_ERR_OVERFLOW = 4, /* nnz(C) does not fit int32 row_ptr */
+    MHS_ERR_IO = 5        /* Matrix Market read failure */
+} mhs_status;
+
+/* A CSR matrix.  For mhs_spgemm the arrays are DEVICE pointers
+ * (the reference's CSR::d_ptr/d_col/d_val, inc/CSR.h:15-17). */
+typedef struct mhs_csr {
+    int32_t M, N, nnz;
+    int32_t *ptr; /* M+1 */
+    int32_t *col; /* nnz */
+    double *val;  /* nnz */
+} mhs_csr;
+
+/* Per-phase times in ms, the reference's Timing fields (inc/Timing.h:3-20),
+ * measured with hipEvents on the context stream, plus the two totals and
+ * run statistics. */
+typedef struct mhs_timing {
+    double mem_alloc;          /* workspace + C.ptr allocation            */
+    double Form_mask_matrix_B; /* B -> (tile col, 64-bit mask) rows       */
+    double symbolic_binning;   /* row analysis + symbolic bins            */
+    double Calculate_C_nnz;    /* symbolic: nnz of every C row            */
+    double numeric_binning;    /* row_ptr scan + numeric bins + readback  */
+    double Malloc_C_col_val;   /* C.col / C.val allocation                */
+    double Numeric;            /* numeric: values + sorted columns        */
+    double total_ref;          /* = getTotal(): all but Form_mask_matrix_B (src/Timing.cpp:39-41) */
+    double total_e2e;          /* everything, device-resident A,B -> device-resident C */
+    uint64_t flop;             /* sum over A's nonzeros of nnz(B row)   (src/main.cu:102-107) */
+    int64_t nnzC;
+    int32_t sym_bins[8];       /* rows per symbolic bin (0: empty rows) */
+    int32_t num_bins[8];       /* rows per numeric bin  (0: empty rows) */
+} mhs_timing;
+
+typedef struct mhs_ctx mhs_ctx;
+
+/* Context = the reference's Tool (inc/Tool.h, src/Tool.cu:4-45): stream,
+ * workspace (kept across calls, grown on demand), pinned readback area.
+ * One context per device; a context is not thread-safe, distinct contexts
+ * may be used from distinct threads. */
+int mhs_ctx_create(mhs_ctx **ctx, int device);
+void mhs_ctx_destroy(mhs_ctx *ctx);
+const char *mhs_last_error(const mhs_ctx *ctx);
+/* Run on a caller-owned hipStream_t (e.g. PyTorch's current stream); NULL
+ * restores the context's own stream. */
+int mhs_ctx_set_stream(mhs_ctx *ctx, void *hip_stream);
+/* Release cached workspace and pooled output buffers. */
+int mhs_ctx_trim(mhs_ctx *ctx);
+
+/* C = A * B on the device.  A, B: device CSR.  On MHS_OK, C->M = A->M,
+ * C->N = B->N, C->nnz is set and C->ptr/col/val are fresh device
+ * allocations owned by the caller (free with mhs_csr_free, or hand back to
+ * the context's pool with mhs_ctx_recycle).  A and B may alias.  B is not
+ * modified (unlike the reference, which allocates B.d_tile* in place).
+ * Returns after C is complete (the context stream is synchronised).
+ * t may be NULL. */
+int mhs_spgemm(mhs_ctx *ctx, const mhs_csr *A, const mhs_csr *B, mhs_csr *C, mhs_timing *t);
+
+/* Free a device CSR produced by mhs_spgemm (hipFree) and zero the struct. */
+void mhs_csr_free(mhs_csr *C);
+/* Return C's device buffers to ctx's output pool for reuse by later calls
+ * (a caching allocator: avoids hipMalloc/hipFree per call). */
+void mhs_ctx_recycle(mhs_ctx *ctx, mhs_csr *C);
+
+/* ---- host-side helpers (the reference's L1 layer) ---------------------- */
+
+/* Host CSR (malloc'ed arrays). */
+typedef struct mhs_host_csr {
+    int32_t M, N, nnz;
+    int32_t *ptr, *col;
+    double *val;
+    int32_t is_symmetric;
+} mhs_host_csr;
+
+/* readMtxFile (inc/mmio_read.h:34-159): real/integer/pattern(1.0)/complex
+ * (real part); symmetric and hermitian off-diagonals mirrored, skew not;
+ * duplicates kept; rows sorted by (col, val).  Returns MHS_OK or MHS_ERR_IO. */
+int mhs_read_mtx(const char *path, mhs_host_csr *A);
+void mhs_host_csr_free(mhs_host_csr *A);
+/* int_result of src/main.cu:102-107. */
+uint64_t mhs_flop_count(int32_t nnzA, const int32_t *Acol, const int32_t *Bptr);
+
+/* Device memory helpers for callers without their own HIP runtime binding
+ * (e.g. ctypes).  kind: 0 = H2D, 1 = D2H, 2 = D2D.  Synchronous on ctx's stream. */
+int mhs_memcpy(mhs_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
+int mhs_device_alloc(mhs_ctx *ctx, void **p, size_t bytes);
+int mhs_device_free(mhs_ctx *ctx, void *p);
+
+int mhs_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MHSPGEMM_H */

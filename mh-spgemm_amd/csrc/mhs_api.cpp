@@ -1,0 +1,429 @@
+// mhs_api.cpp -- C-ABI orchestration of the MI355X SpGEMM (include/mhspgemm.h).
+//
+// Replaces MH_spgemm (reference src/main.cu:12-72) and the Tool workspace
+// (src/Tool.cu:4-69).  One call = one stream-ordered pipeline:
+//
+//   memset stats -> k_mask_b (Form_mask_matrix_B) -> k_analyze + bins (symbolic_binning)
+//   -> symbolic bins (Calculate_C_nnz) -> scan + classify + bins + ONE readback
+//   (numeric_binning) -> C.col/C.val allocation (Malloc_C_col_val) -> numeric bins
+//   (Numeric) -> stream sync.
+//
+// The reference makes 5 binning round trips (2 blocking copies each), 3 scalar
+// reads and 6 device-wide syncs per call; here the only host round
+// trip is the single Stats readback that C's allocation needs anyway.
+#include "mhs_internal.hpp"
+#include "../../include/mhspgemm.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace mhs;
+
+struct mhs_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    char* ws = nullptr;
+    size_t ws_bytes = 0;
+    char* gscratch = nullptr;
+    size_t gscratch_bytes = 0;
+    Stats* h_stats = nullptr;  // pinned
+    hipEvent_t ev[8] = {};
+    // output pool (caching allocator for C arrays)
+    std::vector<std::pair<void*, size_t>> pool;
+    std::unordered_map<void*, size_t> sizes;
+};
+
+namespace {
+
+int fail(mhs_ctx* ctx, int code, const std::string& what) {
+    if (ctx) ctx->err = what;
+    return code;
+}
+
+int fail_hip(mhs_ctx* ctx, hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    (void)hipGetLastError();
+    return fail(ctx, e == hipErrorOutOfMemory ? MHS_ERR_OOM : MHS_ERR_HIP, m);
+}
+
+#define MHS_HIP(expr)                                                   \
+    do {                                                                \
+        hipError_t e_ = (expr);                                         \
+        if (e_ != hipSuccess) return fail_hip(ctx, e_, #expr);          \
+    } while (0)
+
+inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+hipError_t pool_get(mhs_ctx* ctx, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    size_t best = (size_t)-1;
+    size_t bi = 0;
+    for (size_t i = 0; i < ctx->pool.size(); ++i) {
+        const size_t s = ctx->pool[i].second;
+        if (s >= bytes && s <= 2 * bytes + (1u << 20) && s < best) {
+            best = s;
+            bi = i;
+        }
+    }
+    if (best != (size_t)-1) {
+        *p = ctx->pool[bi].first;
+        ctx->pool.erase(ctx->pool.begin() + (long)bi);
+        ctx->sizes[*p] = best;
+        return hipSuccess;
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory && !ctx->pool.empty()) {
+        for (auto& b : ctx->pool) (void)hipFree(b.first);
+        ctx->pool.clear();
+        (void)hipGetLastError();
+        e = hipMalloc(p, bytes);
+    }
+    if (e == hipSuccess) ctx->sizes[*p] = bytes;
+    return e;
+}
+
+void pool_put(mhs_ctx* ctx, void* p) {
+    if (!p) return;
+    auto it = ctx->sizes.find(p);
+    if (it == ctx->sizes.end()) {
+        (void)hipFree(p);
+        return;
+    }
+    ctx->pool.emplace_back(p, it->second);
+    ctx->sizes.erase(it);
+    // keep the pool bounded: drop the oldest buffers beyond 16 entries
+    while (ctx->pool.size() > 16) {
+        (void)hipFree(ctx->pool.front().first);
+        ctx->pool.erase(ctx->pool.begin());
+    }
+}
+
+struct Layout {
+    size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, bin_id, blkcnt, rowlist,
+        scan_part, blkflop, stats, total;
+};
+
+Layout plan(int M, int MB, long long nnzB) {
+    Layout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        size_t r = o;
+        o += al(bytes ? bytes : 16);
+        return r;
+    };
+    const size_t nblk = (size_t)(M + BIN_BLOCK - 1) / BIN_BLOCK + 1;
+    const size_t nscan = (size_t)(M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1;
+    L.stats = take(sizeof(Stats));
+    L.btcol = take((size_t)nnzB * 4);
+    L.btmask = take((size_t)nnzB * 8);
+    L.bmeta = take((size_t)MB * 16);
+    L.bhi = take((size_t)MB * 4);
+    L.rflop = take((size_t)M * 4);
+    L.rtflop = take((size_t)M * 4);
+    L.rlo = take((size_t)M * 4);
+    L.rhi = take((size_t)M * 4);
+    L.ctiles = take((size_t)M * 4);
+    L.bin_id = take((size_t)M);
+    L.blkcnt = take(NBINS * nblk * 4);
+    L.rowlist = take((size_t)M * 4);
+    L.scan_part = take(nscan * 8);
+    L.blkflop = take(((size_t)M / 4 + 16) * 8);
+    L.total = o;
+    return L;
+}
+
+int ensure(mhs_ctx* ctx, char** buf, size_t* have, size_t need) {
+    if (*have >= need) return MHS_OK;
+    if (*buf) {
+        MHS_HIP(hipStreamSynchronize(ctx->stream));
+        MHS_HIP(hipFree(*buf));
+        *buf = nullptr;
+        *have = 0;
+    }
+    const size_t want = need + need / 8;
+    MHS_HIP(hipMalloc((void**)buf, want));
+    *have = want;
+    return MHS_OK;
+}
+
+constexpr int NUM_GLOBAL_GRID = 128;
+
+int sym_global_grid(int N, size_t* bytes) {
+    const size_t per = sym_global_bytes_per_block(N);
+    size_t g = per ? (size_t)(256u << 20) / per : 64;
+    if (g < 1) g = 1;
+    if (g > 64) g = 64;
+    if (g >= 8) g &= ~size_t(7);
+    *bytes = g * per;
+    return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mhs_abi_version(void) { return MHS_ABI_VERSION; }
+
+int mhs_ctx_create(mhs_ctx** out, int device) {
+    if (!out) return MHS_ERR_INVALID;
+    *out = nullptr;
+    mhs_ctx* ctx = new mhs_ctx();
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->h_stats, sizeof(Stats), hipHostMallocDefault);
+    for (int i = 0; e == hipSuccess && i < 8; ++i) e = hipEventCreate(&ctx->ev[i]);
+    if (e != hipSuccess) {
+        fprintf(stderr, "mhs_ctx_create: %s\n", hipGetErrorString(e));
+        delete ctx;
+        return e == hipErrorOutOfMemory ? MHS_ERR_OOM : MHS_ERR_HIP;
+    }
+    ctx->stream = ctx->own_stream;
+    init_kernel_attributes();
+    *out = ctx;
+    return MHS_OK;
+}
+
+void mhs_ctx_destroy(mhs_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    mhs_ctx_trim(ctx);
+    for (auto& kv : ctx->sizes) (void)kv;  // outstanding C buffers belong to the caller
+    if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
+    for (auto& ev : ctx->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+const char* mhs_last_error(const mhs_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int mhs_ctx_set_stream(mhs_ctx* ctx, void* s) {
+    if (!ctx) return MHS_ERR_INVALID;
+    ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    return MHS_OK;
+}
+
+int mhs_ctx_trim(mhs_ctx* ctx) {
+    if (!ctx) return MHS_ERR_INVALID;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->gscratch) (void)hipFree(ctx->gscratch);
+    ctx->ws = ctx->gscratch = nullptr;
+    ctx->ws_bytes = ctx->gscratch_bytes = 0;
+    for (auto& b : ctx->pool) (void)hipFree(b.first);
+    ctx->pool.clear();
+    return MHS_OK;
+}
+
+void mhs_csr_free(mhs_csr* C) {
+    if (!C) return;
+    if (C->ptr) (void)hipFree(C->ptr);
+    if (C->col) (void)hipFree(C->col);
+    if (C->val) (void)hipFree(C->val);
+    std::memset(C, 0, sizeof *C);
+}
+
+void mhs_ctx_recycle(mhs_ctx* ctx, mhs_csr* C) {
+    if (!C) return;
+    if (!ctx) {
+        mhs_csr_free(C);
+        return;
+    }
+    pool_put(ctx, C->ptr);
+    pool_put(ctx, C->col);
+    pool_put(ctx, C->val);
+    std::memset(C, 0, sizeof *C);
+}
+
+int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs_timing* t) {
+    if (!ctx) return MHS_ERR_INVALID;
+    if (!A || !B || !C) return fail(ctx, MHS_ERR_INVALID, "null argument");
+    if (A->M < 0 || A->N < 0 || A->nnz < 0 || B->M < 0 || B->N < 0 || B->nnz < 0)
+        return fail(ctx, MHS_ERR_INVALID, "negative dimension");
+    if (A->N != B->M)
+        return fail(ctx, MHS_ERR_INVALID, "A.N != B.M (C = A*B needs matching inner dimension)");
+    if ((A->M > 0 && !A->ptr) || (B->M > 0 && !B->ptr) || (A->nnz > 0 && (!A->col || !A->val)) ||
+        (B->nnz > 0 && (!B->col || !B->val)))
+        return fail(ctx, MHS_ERR_INVALID, "null device array");
+    MHS_HIP(hipSetDevice(ctx->device));
+    const auto T0 = std::chrono::steady_clock::now();
+    hipStream_t s = ctx->stream;
+    const bool timed = t != nullptr;
+    mhs_timing tm{};
+
+    const int M = A->M, N = B->N, MB = B->M;
+    mhs_csr out{};
+    out.M = M;
+    out.N = N;
+
+    // ---- mem_alloc: workspace (cached across calls) + C.ptr --------------------
+    const Layout L = plan(M, MB, B->nnz);
+    size_t sym_g_bytes = 0;
+    const int sym_grid = sym_global_grid(N, &sym_g_bytes);
+    int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->gscratch, &ctx->gscratch_bytes, sym_g_bytes);
+    if (rc) return rc;
+    MHS_HIP(pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4));
+    Work w{};
+    w.btcol = (int*)(ctx->ws + L.btcol);
+    w.btmask = (unsigned long long*)(ctx->ws + L.btmask);
+    w.bmeta = (int4*)(ctx->ws + L.bmeta);
+    w.bhi = (int*)(ctx->ws + L.bhi);
+    w.rflop = (int*)(ctx->ws + L.rflop);
+    w.rtflop = (int*)(ctx->ws + L.rtflop);
+    w.rlo = (int*)(ctx->ws + L.rlo);
+    w.rhi = (int*)(ctx->ws + L.rhi);
+    w.ctiles = (int*)(ctx->ws + L.ctiles);
+    w.bin_id = (unsigned char*)(ctx->ws + L.bin_id);
+    w.blkcnt = (int*)(ctx->ws + L.blkcnt);
+    w.rowlist = (int*)(ctx->ws + L.rowlist);
+    w.scan_part = (int*)(ctx->ws + L.scan_part);
+    w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
+    w.stats = (Stats*)(ctx->ws + L.stats);
+    w.gscratch = ctx->gscratch;
+    w.gscratch_bytes = ctx->gscratch_bytes;
+    MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
+    if (M == 0) {
+        MHS_HIP(hipMemsetAsync(out.ptr, 0, 4, s));
+    }
+    const double t_alloc = ms_since(T0);
+    if (timed) MHS_HIP(hipEventRecord(ctx->ev[0], s));
+
+    const Csr a{A->M, A->N, A->nnz, A->ptr, A->col, A->val};
+    const Csr b{B->M, B->N, B->nnz, B->ptr, B->col, B->val};
+
+    // ---- Form_mask_matrix_B ------------------------------------------------------
+    launch_mask_b(b, w, s);
+    if (timed) MHS_HIP(hipEventRecord(ctx->ev[1], s));
+    // ---- symbolic_binning ---------------------------------------------------------
+    const int nflop_blocks = launch_analyze(a, w, MB, s, out.ptr);
+    launch_binning(M, w, 0, s, nflop_blocks);
+    if (timed) MHS_HIP(hipEventRecord(ctx->ev[2], s));
+    // ---- Calculate_C_nnz ------------------------------------------------------------
+    launch_symbolic(a, w, M, N, out.ptr, s, sym_grid);
+    if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
+    // ---- numeric_binning: scan, classify, bins, one readback ------------------------
+    if (M > 0) {
+        launch_scan_classify(M, w, out.ptr, s);
+        launch_binning(M, w, 1, s, 0);
+    }
+    MHS_HIP(hipGetLastError());
+    MHS_HIP(hipMemcpyAsync(ctx->h_stats, w.stats, sizeof(Stats), hipMemcpyDeviceToHost, s));
+    if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
+    MHS_HIP(hipStreamSynchronize(s));
+    const Stats h = *ctx->h_stats;
+    if (h.err) {
+        pool_put(ctx, out.ptr);
+        std::string m;
+        if (h.err & ERR_UNSORTED) m += "B column indices are not sorted within a row; ";
+        if (h.err & ERR_COL_RANGE) m += "B column index out of [0, B.N); ";
+        if (h.err & ERR_ACOL_RANGE) m += "A column index out of [0, B.M); ";
+        if (h.err & ERR_OVERFLOW) m += "nnz(C) exceeds INT32_MAX; ";
+        return fail(ctx, (h.err & ERR_OVERFLOW) ? MHS_ERR_OVERFLOW : MHS_ERR_INVALID, m);
+    }
+    out.nnz = (int)h.nnzC;
+
+    // ---- Malloc_C_col_val ---------------------------------------------------------------
+    const auto T5 = std::chrono::steady_clock::now();
+    {
+        hipError_t e = pool_get(ctx, (void**)&out.col, (size_t)out.nnz * 4);
+        if (e == hipSuccess) e = pool_get(ctx, (void**)&out.val, (size_t)out.nnz * 8);
+        if (e != hipSuccess) {
+            pool_put(ctx, out.ptr);
+            pool_put(ctx, out.col);
+            return fail_hip(ctx, e, "allocating C.col/C.val");
+        }
+    }
+    if (h.num_count[NUM_GLOBAL] > 0) {
+        const size_t per = (size_t)align16(h.num_global_need);
+        const size_t g = (size_t)std::min(h.num_count[NUM_GLOBAL], NUM_GLOBAL_GRID);
+        rc = ensure(ctx, &ctx->gscratch, &ctx->gscratch_bytes, per * g);
+        if (rc) {
+            mhs_ctx_recycle(ctx, &out);
+            return rc;
+        }
+        w.gscratch = ctx->gscratch;
+        w.gscratch_bytes = ctx->gscratch_bytes;
+    }
+    const double t_malloc = ms_since(T5);
+
+    // ---- Numeric -------------------------------------------------------------------------
+    if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
+    if (out.nnz > 0) launch_numeric(a, b, w, h, out.ptr, out.col, out.val, s, NUM_GLOBAL_GRID);
+    MHS_HIP(hipGetLastError());
+    if (timed) MHS_HIP(hipEventRecord(ctx->ev[6], s));
+    MHS_HIP(hipStreamSynchronize(s));
+    *C = out;
+
+    if (timed) {
+        float f = 0;
+        tm.mem_alloc = t_alloc;
+        MHS_HIP(hipEventElapsedTime(&f, ctx->ev[0], ctx->ev[1]));
+        tm.Form_mask_matrix_B = f;
+        MHS_HIP(hipEventElapsedTime(&f, ctx->ev[1], ctx->ev[2]));
+        tm.symbolic_binning = f;
+        MHS_HIP(hipEventElapsedTime(&f, ctx->ev[2], ctx->ev[3]));
+        tm.Calculate_C_nnz = f;
+        MHS_HIP(hipEventElapsedTime(&f, ctx->ev[3], ctx->ev[4]));
+        tm.numeric_binning = f;
+        tm.Malloc_C_col_val = t_malloc;
+        MHS_HIP(hipEventElapsedTime(&f, ctx->ev[5], ctx->ev[6]));
+        tm.Numeric = f;
+        tm.total_e2e = ms_since(T0);
+        tm.total_ref = tm.total_e2e - tm.Form_mask_matrix_B;
+        tm.flop = h.flop;
+        tm.nnzC = h.nnzC;
+        for (int i = 0; i < 8; ++i) {
+            tm.sym_bins[i] = i < NBINS ? h.sym_count[i] : 0;
+            tm.num_bins[i] = i < NBINS ? h.num_count[i] : 0;
+        }
+        long long nonempty = 0;
+        for (int i = 1; i < NBINS; ++i) nonempty += h.sym_count[i];
+        tm.sym_bins[0] = (int)(M - nonempty);
+        nonempty = 0;
+        for (int i = 1; i < NBINS; ++i) nonempty += h.num_count[i];
+        tm.num_bins[0] = (int)(M - nonempty);
+        *t = tm;
+    }
+    return MHS_OK;
+}
+
+int mhs_memcpy(mhs_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {
+    if (!ctx) return MHS_ERR_INVALID;
+    if (bytes == 0) return MHS_OK;
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    MHS_HIP(hipSetDevice(ctx->device));
+    MHS_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->stream));
+    MHS_HIP(hipStreamSynchronize(ctx->stream));
+    return MHS_OK;
+}
+
+int mhs_device_alloc(mhs_ctx* ctx, void** p, size_t bytes) {
+    if (!ctx || !p) return MHS_ERR_INVALID;
+    MHS_HIP(hipSetDevice(ctx->device));
+    MHS_HIP(hipMalloc(p, bytes ? bytes : 16));
+    return MHS_OK;
+}
+
+int mhs_device_free(mhs_ctx* ctx, void* p) {
+    if (!ctx) return MHS_ERR_INVALID;
+    if (p) MHS_HIP(hipFree(p));
+    return MHS_OK;
+}
+
+}  // extern "C"

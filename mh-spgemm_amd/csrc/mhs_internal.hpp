@@ -1,0 +1,164 @@
+// mhs_internal.hpp -- shared host/device declarations of the MI355X SpGEMM.
+//
+// Layout in HBM (all arrays live in the context workspace unless noted):
+//   B side (per B row r, built by k_mask_b = Form_mask_matrix_B):
+//     btcol[nnzB]  int32   tile column (col >> 6) of each 64-column tile of row r,
+//     btmask[nnzB] uint64  bitmask of the row's columns inside that tile;
+//                          row r's tiles sit at [B.ptr[r], B.ptr[r] + ntiles(r)),
+//                          i.e. the tile arrays reuse B's own row_ptr (tiles(r) <= nnz(r)),
+//                          so no scan and no second pass are needed.
+//     bmeta[MB]    int4    {tile start (= B.ptr[r]), nnz(r), ntiles(r), lo tile}
+//     bhi[MB]      int32   hi tile (lo = INT_MAX / hi = -1 for empty rows)
+//   C side (per C row i, built by k_analyze):
+//     rflop[M]  products of row i (saturated int32)   = the reference's "flop"
+//     rtflop[M] tile products of row i               = the reference's "tile-flop"
+//     rlo/rhi   tile span of row i
+//     ctiles[M] distinct C tiles of row i (symbolic)
+//     C.ptr     nnz of row i (symbolic), then scanned in place to the row_ptr
+//   binning: bin id per row (uint8), per-block bin counts, row lists grouped by bin.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mhs {
+
+constexpr int TILE_SHIFT = 6;  // 64-column tiles, one uint64 mask each (wave64 ballot width)
+constexpr int TILE_BITS = 64;
+constexpr int NBINS = 8;
+constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
+constexpr int BIN_BLOCK = 1024; // rows per block in the binning kernels
+constexpr int SCAN_ITEMS = 4096;// rows per block in the row_ptr scan
+
+// Symbolic bins (by LDS need and tile work).
+enum SymBin : int { SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_NB = 5 };
+// Numeric bins (by LDS need and product work).
+enum NumBin : int {
+    NUM_NONE = 0, NUM_W4 = 1, NUM_W16 = 2, NUM_B256 = 3, NUM_B1024 = 4, NUM_GLOBAL = 5, NUM_NB = 6
+};
+
+// Per-team LDS budgets (bytes).  The wave kernels carve one region per wave.
+constexpr int SYM_WAVE_BYTES = 4096;
+constexpr int SYM_WAVE_WORK = 4096;     // tile products a single wave takes on
+constexpr int SYM_B256_BYTES = 32768;
+constexpr int SYM_B256_WORK = 1 << 20;
+constexpr int NUM_W4_BYTES = 4096;
+constexpr int NUM_W4_WORK = 8192;       // products a single wave takes on
+constexpr int NUM_W16_BYTES = 16384;
+constexpr int NUM_W16_WORK = 32768;
+constexpr int NUM_B256_BYTES = 65536;
+constexpr int NUM_B256_WORK = 1 << 22;
+constexpr int LDS_MAX = 163840;         // gfx950: 160 KiB per workgroup (probed on the box)
+constexpr int BLOCK_HDR = 2048;         // per-block LDS header: reductions, counter, A-entry stage
+constexpr int WAVE_HDR = 16;            // per-wave LDS header
+constexpr int B1024_BYTES = LDS_MAX - BLOCK_HDR - 1024;  // budget of the 1024-thread kernels
+
+// One 16-byte tile-table entry: OR of the masks of every B tile that maps to
+// this C tile, the C-row rank of its first column, and the key (hash mode).
+struct alignas(16) TileEntry {
+    unsigned long long mask;
+    int base;
+    int key;
+};
+
+// Device-side statistics read back once per call (the only mid-call sync).
+struct Stats {
+    unsigned long long flop;       // total products
+    long long nnzC;                // total C nnz (scan result)
+    int err;                       // error bits (ERR_*)
+    int pad0;
+    int sym_count[NBINS];
+    int num_count[NBINS];
+    int num_global_need;           // max LDS-equivalent bytes of a global numeric row
+    int pad1;
+    long long sym_start[NBINS];
+    long long num_start[NBINS];
+};
+constexpr int ERR_UNSORTED = 1;
+constexpr int ERR_COL_RANGE = 2;
+constexpr int ERR_ACOL_RANGE = 4;
+constexpr int ERR_OVERFLOW = 8;
+
+__host__ __device__ inline int next_pow2(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+__host__ __device__ inline int ilog2(int x) {  // x power of two
+    int l = 0;
+    while ((1 << l) < x) ++l;
+    return l;
+}
+// Open-addressed table size for up to `bound` distinct keys: load <= 1/2.
+__host__ __device__ inline int hash_slots(int bound) {
+    int h = next_pow2(2 * (bound < 1 ? 1 : bound));
+    return h < 16 ? 16 : h;
+}
+__host__ __device__ inline long long align16(long long x) { return (x + 15) & ~15LL; }
+
+// Symbolic tile table: direct-mapped over the row's tile span, or hashed.
+__host__ __device__ inline bool sym_direct(int span, int tflop) {
+    int bound = tflop < span ? tflop : span;
+    return span <= hash_slots(bound);
+}
+__host__ __device__ inline long long sym_need(int span, int tflop) {
+    int bound = tflop < span ? tflop : span;
+    int e = sym_direct(span, tflop) ? span : hash_slots(bound);
+    return (long long)e * 16;
+}
+// Numeric: tile table (direct or hash) + accumulator / sort region.
+__host__ __device__ inline bool num_direct(int span, int t, int n) {
+    long long nd = (long long)span * 16 + align16((long long)n * 8);
+    int h = hash_slots(t);
+    int p = next_pow2(t);
+    long long nh = (long long)h * 16 + align16((long long)(n > p ? n : p) * 8);
+    return nd <= nh;
+}
+__host__ __device__ inline long long num_need(int span, int t, int n) {
+    if (num_direct(span, t, n)) return (long long)span * 16 + align16((long long)n * 8);
+    int h = hash_slots(t);
+    int p = next_pow2(t);
+    return (long long)h * 16 + align16((long long)(n > p ? n : p) * 8);
+}
+
+// ------------------------------------------------------------ launchers ---
+struct Csr {
+    int M, N, nnz;
+    const int* ptr;
+    const int* col;
+    const double* val;
+};
+
+struct Work {
+    // B side
+    int* btcol;
+    unsigned long long* btmask;
+    int4* bmeta;
+    int* bhi;
+    // C side
+    int* rflop;
+    int* rtflop;
+    int* rlo;
+    int* rhi;
+    int* ctiles;
+    unsigned char* bin_id;
+    int* blkcnt;       // NBINS * nblk
+    int* rowlist;      // M
+    int* scan_part;    // block sums of the row_ptr scan (long long stored as 2 ints)
+    unsigned long long* blkflop;  // per-block flop partials of k_analyze
+    Stats* stats;
+    void* gscratch;    // global-bin scratch
+    size_t gscratch_bytes;
+};
+
+void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);
+int launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr);  // returns #blocks
+void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks);  // phase 0 sym, 1 num
+void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s,
+                     int global_grid);
+void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s);
+void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
+                    int* Ccol, double* Cval, hipStream_t s, int global_grid);
+size_t sym_global_bytes_per_block(int N);
+void init_kernel_attributes();
+
+}  // namespace mhs

@@ -1,0 +1,1101 @@
+// mhs_kernels.hip -- gfx950 (MI355X, CDNA4) kernels of the mask-and-hash SpGEMM.
+//
+// Phases (reference call path src/main.cu:12-72, inc/MH_spgemm.cuh):
+//   k_mask_b          Form_mask_matrix_B (MH_spgemm.cuh:242-295, Form_mask_matrix_B.cuh):
+//                     every B row -> (64-column tile, 64-bit mask) pairs.  Columns are
+//                     sorted, so a tile is a run of equal col>>6 found with one wave
+//                     ballot + a segmented OR scan per 64 entries: no hash, one pass,
+//                     written in place of the row's own CSR slots (no scan, no malloc).
+//   k_analyze         flop / tile-flop / tile span per A row (k_calculate_flop,
+//                     Form_mask_matrix_B.cuh:14-95) + symbolic bin id.
+//   k_bin_*           stable row binning (binning.cuh:67-155) without host round trips.
+//   k_sym_*           Calculate_C_nnz (MH_spgemm.cuh:297-362, Calculate_C_nnz.cuh):
+//                     OR the B tile masks of a C row into an LDS tile table (direct-
+//                     mapped over the row's tile span, or open-addressed), nnz = sum popc.
+//   k_scan_*          row_ptr exclusive scan (CUB ExclusiveSum, src/main.cu:55) fused
+//                     with the numeric bin classification.
+//   k_num_*           h_numeric (MH_spgemm.cuh:364-430, numeric.cuh): rebuild the C
+//                     row's tile table, give every tile the C-row rank of its first
+//                     column (prefix popcount in tile order), then every product
+//                     lands at base + popc(mask & below(col)) in a dense LDS
+//                     accumulator: no key CAS per product and no sort of the output,
+//                     columns come out ordered by construction.
+//
+// Every phase is binned by row size into wave-per-row kernels (one LDS region per
+// wave, no block barriers), block-per-row kernels (256 / 1024 threads, up to 160 KiB
+// of LDS) and a global-memory fallback; rows are walked in XCD-grouped order so that
+// neighbouring rows (which share B rows) run on one XCD's L2.
+#include "mhs_internal.hpp"
+
+#include <climits>
+
+namespace mhs {
+
+// ------------------------------------------------------------------ helpers ---
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Ordering point for LDS traffic between lanes of ONE wave: a wave's LDS
+// operations are performed in issue order, so only the compiler must be kept
+// from moving accesses across this point.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class V>
+__device__ __forceinline__ V wave_sum(V v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ long long wave_incl_scan64(long long x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        long long y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    const int lane = lane_id();
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__device__ __forceinline__ int hslot(int key, int shift) {
+    return (int)(((unsigned)key * 2654435769u) >> (32 - shift));
+}
+
+__device__ __forceinline__ int sat_int(long long x) { return x > INT_MAX ? INT_MAX : (int)x; }
+
+// Lane-group width for walking the products of one row: groups of G lanes
+// take one A entry each and stride its B row.  Pick G minimising the sweeps
+// ceil(nA / groups) * ceil(avg B-row length / G) (ties -> wider, better
+// coalesced groups); at most 64 groups so one staged chunk of 64 A entries
+// feeds every group.
+__device__ __forceinline__ int pick_group(long long work, int nA, int T) {
+    int gmin = T / 64;
+    if (gmin < 4) gmin = 4;
+    if (nA <= 0) return gmin;
+    const long long avg = (work + nA - 1) / nA;
+    int best = gmin;
+    long long bc = LLONG_MAX;
+    for (int g = gmin; g <= T; g <<= 1) {
+        const int ng = T / g;
+        const long long c = (long long)((nA + ng - 1) / ng) * ((avg + g - 1) / g);
+        if (c <= bc) {
+            bc = c;
+            best = g;
+        }
+    }
+    return best;
+}
+
+// XCD-grouped walk over a row list: blocks b and b+8 share an XCD (round-robin
+// dispatch), so group g = b % 8 takes the g-th eighth of the list and its blocks
+// stride through it.  Speed only -- any placement gives the same result.
+struct RowWalk {
+    int first, end, stride;
+    __device__ RowWalk(int count, int teams_per_block, int team) {
+        if ((gridDim.x & 7) == 0) {
+            const int g = blockIdx.x & 7, nbg = gridDim.x >> 3, bi = blockIdx.x >> 3;
+            first = (int)((long long)count * g / 8) + bi * teams_per_block + team;
+            end = (int)((long long)count * (g + 1) / 8);
+            stride = nbg * teams_per_block;
+        } else {
+            first = blockIdx.x * teams_per_block + team;
+            end = count;
+            stride = gridDim.x * teams_per_block;
+        }
+    }
+};
+
+// ------------------------------------------------------------------- teams ---
+// A team processes one row at a time: a wave (64 lanes, wave_sync) or a whole
+// block (__syncthreads; reductions through an LDS header).  GlobalTeam is a
+// block whose tables live in global memory: its sync makes global stores and
+// atomics visible block-wide (agent-scope fence: L1 invalidate).
+
+struct WaveTeam {
+    static constexpr int size = 64;
+    __device__ int rank() const { return lane_id(); }
+    __device__ void sync() const { wave_sync(); }
+    template <class V>
+    __device__ V sum(V v) const { return wave_sum(v); }
+    template <class LD, class ST>
+    __device__ void exclusive_scan(int L, LD load, ST store) const {
+        const int lane = lane_id();
+        int carry = 0;
+        for (int b = 0; b < L; b += 64) {
+            const int i = b + lane;
+            const int x = i < L ? load(i) : 0;
+            const int inc = wave_incl_scan(x);
+            if (i < L) store(i, carry + inc - x);
+            carry += __shfl(inc, 63);
+        }
+    }
+};
+
+template <int T, bool GLOBALMEM>
+struct BlockTeam {
+    static constexpr int size = T;
+    static constexpr int W = T / 64;
+    long long* scratch;  // LDS, >= W entries
+    __device__ int rank() const { return threadIdx.x; }
+    __device__ void sync() const {
+        if constexpr (GLOBALMEM) __threadfence();
+        __syncthreads();
+    }
+    template <class V>
+    __device__ V sum(V v) const {
+        v = wave_sum(v);
+        const int w = threadIdx.x >> 6;
+        if (lane_id() == 0) scratch[w] = (long long)v;
+        __syncthreads();
+        long long r = 0;
+#pragma unroll
+        for (int i = 0; i < W; ++i) r += scratch[i];
+        __syncthreads();
+        return (V)r;
+    }
+    template <class LD, class ST>
+    __device__ void exclusive_scan(int L, LD load, ST store) const {
+        const int lane = lane_id(), w = threadIdx.x >> 6;
+        int* ws = (int*)scratch;
+        int carry = 0;
+        for (int b = 0; b < L; b += T) {
+            const int i = b + (int)threadIdx.x;
+            const int x = i < L ? load(i) : 0;
+            const int inc = wave_incl_scan(x);
+            if (lane == 63) ws[w] = inc;
+            __syncthreads();
+            int woff = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                const int v = ws[k];
+                woff += (k < w) ? v : 0;
+                tot += v;
+            }
+            if (i < L) store(i, carry + woff + inc - x);
+            carry += tot;
+            __syncthreads();
+        }
+        if constexpr (GLOBALMEM) sync();
+    }
+};
+
+template <class Team>
+__device__ void team_bitonic(const Team& tm, unsigned long long* S, int P) {
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tm.rank(); i < P; i += Team::size) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long a = S[i], b = S[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        S[i] = b;
+                        S[ixj] = a;
+                    }
+                }
+            }
+            tm.sync();
+        }
+    }
+}
+
+template <bool GLOBALMEM>
+__device__ __forceinline__ void acc_add(double* p, double v) {
+    if constexpr (GLOBALMEM) unsafeAtomicAdd(p, v);
+    else atomicAdd(p, v);  // ds_add_f64
+}
+
+// --------------------------------------------------- Form_mask_matrix_B ---
+// G lanes per B row.  Per chunk of G entries: head = first entry of a tile run,
+// a forward segmented OR scan collects each run's bits, the run's last lane
+// (tail) writes (tile, mask) at row_start + run index.  A run that crosses a
+// chunk edge is carried in `carry`.  Also checks the sorted-columns precondition.
+template <int G>
+__global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __restrict__ ptr,
+                                                const int* __restrict__ col, int* __restrict__ btcol,
+                                                unsigned long long* __restrict__ btmask,
+                                                int4* __restrict__ bmeta, int* __restrict__ bhi,
+                                                Stats* __restrict__ stats) {
+    const int lane = lane_id();
+    const int gl = lane & (G - 1);
+    const int gbase = lane & ~(G - 1);
+    const unsigned long long gmask = (G == 64) ? ~0ull : (((1ull << G) - 1) << gbase);
+    const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
+    const bool valid = row < MB;
+    const int s = valid ? ptr[row] : 0;
+    const int e = valid ? ptr[row + 1] : 0;
+    int ntiles = 0, prev_col = -1, err = 0;
+    unsigned long long carry = 0;
+    for (int b = s; b < e; b += G) {
+        const int j = b + gl;
+        const bool in = j < e;
+        const int c = in ? col[j] : INT_MAX;
+        const int up = __shfl_up(c, 1, G);
+        const int pc = (gl == 0) ? prev_col : up;
+        const int tile = c >> TILE_SHIFT;
+        const int ptile = pc < 0 ? -1 : (pc >> TILE_SHIFT);
+        const bool head = in && tile != ptile;
+        if (in && c < pc) err |= ERR_UNSORTED;
+        if (in && (c < 0 || c >= N)) err |= ERR_COL_RANGE;
+        // next entry's column: within the chunk from the neighbour lane, at the
+        // chunk edge from memory
+        const int dn = __shfl_down(c, 1, G);
+        int nc = (gl == G - 1) ? ((j + 1 < e) ? col[j + 1] : INT_MAX) : dn;
+        if (j + 1 >= e) nc = INT_MAX;
+        const bool tail = in && ((nc >> TILE_SHIFT) != tile || nc == INT_MAX);
+        // forward segmented OR within the chunk
+        unsigned long long m = in ? (1ull << (c & (TILE_BITS - 1))) : 0ull;
+        if (gl == 0 && !head) m |= carry;
+#pragma unroll
+        for (int d = 1; d < G; d <<= 1) {
+            const unsigned long long om = __shfl_up(m, d, G);
+            const int ot = __shfl_up(tile, d, G);
+            if (gl >= d && ot == tile) m |= om;
+        }
+        const unsigned long long hb = __ballot(head) & gmask;
+        if (tail) {
+            const unsigned long long le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+            const int pos = s + ntiles + __popcll(hb & le) - 1;
+            btcol[pos] = tile;
+            btmask[pos] = m;
+        }
+        ntiles += __popcll(hb);
+        const int last = (e - b < G ? e - b : G) - 1;
+        const unsigned long long lm = __shfl(m, gbase + last);
+        const int lc = __shfl(c, gbase + last);
+        const bool lt = __shfl((int)tail, gbase + last) != 0;
+        carry = lt ? 0ull : lm;
+        prev_col = lc;
+    }
+    if (valid && gl == 0) {
+        bmeta[row] = make_int4(s, e - s, ntiles, e > s ? (col[s] >> TILE_SHIFT) : INT_MAX);
+        bhi[row] = e > s ? (col[e - 1] >> TILE_SHIFT) : -1;
+    }
+    if (__any(err != 0)) {
+        int werr = err;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) werr |= __shfl_xor(werr, d);
+        if (lane == 0) atomicOr(&stats->err, werr);
+    }
+}
+
+// ------------------------------------------------------------ row analysis ---
+
+__device__ __forceinline__ int sym_bin_of(int flop, int tflop, int span) {
+    if (flop == 0) return SYM_NONE;
+    const long long need = sym_need(span, tflop);
+    if (need <= SYM_WAVE_BYTES - WAVE_HDR && tflop <= SYM_WAVE_WORK) return SYM_WAVE;
+    if (need <= SYM_B256_BYTES - BLOCK_HDR && tflop <= SYM_B256_WORK) return SYM_B256;
+    if (need <= B1024_BYTES) return SYM_B1024;
+    return SYM_GLOBAL;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __restrict__ Aptr,
+                                                 const int* __restrict__ Acol,
+                                                 const int4* __restrict__ bmeta,
+                                                 const int* __restrict__ bhi, int* __restrict__ rflop,
+                                                 int* __restrict__ rtflop, int* __restrict__ rlo,
+                                                 int* __restrict__ rhi, int* __restrict__ ctiles,
+                                                 unsigned char* __restrict__ bin_id,
+                                                 int* __restrict__ Cptr,
+                                                 unsigned long long* __restrict__ blkflop,
+                                                 Stats* __restrict__ stats) {
+    const int lane = lane_id();
+    const int gl = lane & (G - 1);
+    const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
+    const bool valid = row < M;
+    long long flop = 0, tflop = 0;
+    int lo = INT_MAX, hi = -1, err = 0;
+    if (valid) {
+        const int s = Aptr[row], e = Aptr[row + 1];
+        for (int j = s + gl; j < e; j += G) {
+            const int k = Acol[j];
+            if (k < 0 || k >= MB) {
+                err = ERR_ACOL_RANGE;
+                continue;
+            }
+            const int4 m = bmeta[k];
+            flop += m.y;
+            tflop += m.z;
+            lo = min(lo, m.w);
+            hi = max(hi, bhi[k]);
+        }
+    }
+#pragma unroll
+    for (int d = G / 2; d >= 1; d >>= 1) {
+        flop += __shfl_xor(flop, d);
+        tflop += __shfl_xor(tflop, d);
+        lo = min(lo, __shfl_xor(lo, d));
+        hi = max(hi, __shfl_xor(hi, d));
+    }
+    if (valid && gl == 0) {
+        const int f = sat_int(flop), tf = sat_int(tflop);
+        const int span = f ? hi - lo + 1 : 0;
+        rflop[row] = f;
+        rtflop[row] = tf;
+        rlo[row] = lo;
+        rhi[row] = hi;
+        const int bin = sym_bin_of(f, tf, span);
+        bin_id[row] = (unsigned char)bin;
+        if (bin == SYM_NONE) {
+            Cptr[row] = 0;
+            ctiles[row] = 0;
+        }
+    }
+    // per-block flop partial (one plain store per block; reduced in k_bin_offsets)
+    __shared__ unsigned long long wsum[4];
+    unsigned long long mine = (valid && gl == 0) ? (unsigned long long)flop : 0ull;
+    mine = wave_sum(mine);
+    if (lane == 0) wsum[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) blkflop[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (__any(err != 0) && lane == 0) atomicOr(&stats->err, ERR_ACOL_RANGE);
+}
+
+// ----------------------------------------------------------------- binning ---
+// Stable partition of rows [0, M) by bin id into one list, bin-major.
+
+__global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(int M, int nb, int nblk,
+                                                         const unsigned char* __restrict__ bin_id,
+                                                         int* __restrict__ blkcnt) {
+    __shared__ int cnt[NBINS];
+    if (threadIdx.x < NBINS) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * BIN_BLOCK + threadIdx.x;
+    const int id = i < M ? bin_id[i] : 0;
+    for (int x = 1; x < nb; ++x) {
+        const int c = __popcll(__ballot(id == x));
+        if (lane_id() == 0 && c) atomicAdd(&cnt[x], c);
+    }
+    __syncthreads();
+    if (threadIdx.x < nb) blkcnt[threadIdx.x * nblk + blockIdx.x] = threadIdx.x == 0 ? 0 : cnt[threadIdx.x];
+}
+
+// One block: exclusive scan over blkcnt (bin-major), per-bin count / start.
+__global__ __launch_bounds__(1024) void k_bin_offsets(int nb, int nblk, int* __restrict__ blkcnt,
+                                                      int* __restrict__ out_count,
+                                                      long long* __restrict__ out_start,
+                                                      const unsigned long long* __restrict__ blkflop,
+                                                      int nflop, unsigned long long* __restrict__ out_flop) {
+    __shared__ int ws[16];
+    __shared__ int bintot[NBINS];
+    __shared__ unsigned long long fs[16];
+    if (nflop > 0) {  // total products = sum of k_analyze's per-block partials
+        unsigned long long f = 0;
+        for (int i = threadIdx.x; i < nflop; i += 1024) f += blkflop[i];
+        f = wave_sum(f);
+        if (lane_id() == 0) fs[threadIdx.x >> 6] = f;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long t = 0;
+            for (int k = 0; k < 16; ++k) t += fs[k];
+            *out_flop = t;
+        }
+    }
+    const int L = nb * nblk;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x < NBINS) bintot[threadIdx.x] = 0;
+    __syncthreads();
+    int carry = 0;
+    for (int b = 0; b < L; b += 1024) {
+        const int i = b + threadIdx.x;
+        const int x = i < L ? blkcnt[i] : 0;
+        if (i < L && x) atomicAdd(&bintot[i / nblk], x);
+        const int inc = wave_incl_scan(x);
+        if (lane == 63) ws[w] = inc;
+        __syncthreads();
+        int woff = 0, tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            const int v = ws[k];
+            woff += (k < w) ? v : 0;
+            tot += v;
+        }
+        if (i < L) blkcnt[i] = carry + woff + inc - x;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x < NBINS) {
+        const int x = threadIdx.x;
+        out_count[x] = x < nb ? bintot[x] : 0;
+        out_start[x] = x < nb ? (long long)blkcnt[x * nblk] : 0;
+    }
+}
+
+__global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(int M, int nb, int nblk,
+                                                           const unsigned char* __restrict__ bin_id,
+                                                           const int* __restrict__ blkoff,
+                                                           int* __restrict__ list) {
+    __shared__ int wcnt[NBINS][BIN_BLOCK / 64];
+    const int w = threadIdx.x >> 6;
+    const int i = blockIdx.x * BIN_BLOCK + threadIdx.x;
+    const int id = i < M ? bin_id[i] : 0;
+    int myrank = 0;
+    for (int x = 1; x < nb; ++x) {
+        const unsigned long long bal = __ballot(id == x);
+        if (id == x) myrank = __popcll(bal & lanemask_lt());
+        if (lane_id() == 0) wcnt[x][w] = __popcll(bal);
+    }
+    __syncthreads();
+    if (id > 0 && i < M) {
+        int off = blkoff[id * nblk + blockIdx.x];
+        for (int k = 0; k < w; ++k) off += wcnt[id][k];
+        list[off + myrank] = i;
+    }
+}
+
+// ------------------------------------------------------- product walking ---
+// for_products(team, A row [a0, a1), ...) calls f.put(f.load(idx), a_ij) for
+// every entry idx of the B segment of every A entry j: the B row's CSR range
+// (numeric) or its tile range (tiles == true).  A entries come in chunks of 64
+// loaded with one coalesced gather (A.col, A.val, bmeta[k]); a wave hands them
+// to its lane groups with shuffles, a block through a 1 KiB LDS stage.  Each
+// lane issues two independent B loads before consuming them.
+
+template <class F>
+__device__ __forceinline__ void run_segment(const F& f, int s, int n, int gl, int G, double a) {
+    int q = gl;
+    for (; q + G < n; q += 2 * G) {
+        const auto x = f.load(s + q);
+        const auto y = f.load(s + q + G);
+        f.put(x, a);
+        f.put(y, a);
+    }
+    if (q < n) f.put(f.load(s + q), a);
+}
+
+template <class F>
+__device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
+                                             const int* __restrict__ Acol,
+                                             const double* __restrict__ Aval,
+                                             const int4* __restrict__ bmeta, bool tiles, int G,
+                                             const F& f, int4*) {
+    const int lane = lane_id();
+    const int grp = lane / G, gl = lane & (G - 1), ngrp = 64 / G;
+    for (int jb = a0; jb < a1; jb += 64) {
+        const int jl = jb + lane;
+        int st = 0, ln = 0;
+        double av = 0.0;
+        if (jl < a1) {
+            const int k = Acol[jl];
+            const int4 m = bmeta[k];
+            st = m.x;
+            ln = tiles ? m.z : m.y;
+            if (Aval) av = Aval[jl];
+        }
+        const int nloc = min(64, a1 - jb);
+        const int iters = (nloc + ngrp - 1) / ngrp;
+        for (int it = 0; it < iters; ++it) {
+            const int e = it * ngrp + grp;  // all lanes active at the shuffles
+            const int s = __shfl(st, e);
+            const int n = __shfl(ln, e);    // 0 for e >= nloc (lane e had no entry)
+            const double a = __shfl(av, e);
+            run_segment(f, s, n, gl, G, a);
+        }
+    }
+}
+
+template <int T, bool GM, class F>
+__device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, int a1,
+                                             const int* __restrict__ Acol,
+                                             const double* __restrict__ Aval,
+                                             const int4* __restrict__ bmeta, bool tiles, int G,
+                                             const F& f, int4* stage) {
+    const int grp = threadIdx.x / G, gl = threadIdx.x & (G - 1), ngrp = T / G;  // ngrp <= 64
+    for (int jb = a0; jb < a1; jb += 64) {
+        if (threadIdx.x < 64) {
+            const int jl = jb + threadIdx.x;
+            int4 v = make_int4(0, 0, 0, 0);
+            if (jl < a1) {
+                const int k = Acol[jl];
+                const int4 m = bmeta[k];
+                const double av = Aval ? Aval[jl] : 0.0;
+                v = make_int4(m.x, tiles ? m.z : m.y, __double2loint(av), __double2hiint(av));
+            }
+            stage[threadIdx.x] = v;
+        }
+        __syncthreads();
+        const int nloc = min(64, a1 - jb);
+        for (int e = grp; e < nloc; e += ngrp) {
+            const int4 v = stage[e];
+            run_segment(f, v.x, v.y, gl, G, __hiloint2double(v.w, v.z));
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------- tile tables ---
+// Insert every B tile of the row's products into the tile table E:
+//   direct: slot = tile - lo (the row's tile span), keys implicit;
+//   hash:   open addressing, Fibonacci hash, linear probe, CAS on the key.
+// Tables hold >= 2x the distinct tiles, so an insert always finds a slot.
+struct TileBuild {
+    TileEntry* E;
+    bool direct;
+    int lo, H, hshift;
+    const int* __restrict__ btcol;
+    const unsigned long long* __restrict__ btmask;
+    struct Item {
+        int tc;
+        unsigned long long m;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{btcol[i], btmask[i]}; }
+    __device__ __forceinline__ void put(const Item& x, double) const {
+        if (direct) {
+            atomicOr(&E[x.tc - lo].mask, x.m);
+        } else {
+            int s = hslot(x.tc, hshift);
+            for (;;) {
+                const int old = atomicCAS(&E[s].key, -1, x.tc);
+                if (old == -1 || old == x.tc) {
+                    atomicOr(&E[s].mask, x.m);
+                    break;
+                }
+                s = (s + 1) & (H - 1);
+            }
+        }
+    }
+};
+
+// Numeric: product (c, a*b) -> acc[base(tile(c)) + popc(mask & below(c))].
+template <bool GM>
+struct Accum {
+    const TileEntry* E;
+    double* acc;
+    bool direct;
+    int lo, H, hshift;
+    const int* __restrict__ Bcol;
+    const double* __restrict__ Bval;
+    struct Item {
+        int c;
+        double v;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{Bcol[i], Bval[i]}; }
+    __device__ __forceinline__ void put(const Item& x, double a) const {
+        const int tc = x.c >> TILE_SHIFT;
+        int s;
+        if (direct) {
+            s = tc - lo;
+        } else {
+            s = hslot(tc, hshift);
+            while (E[s].key != tc) s = (s + 1) & (H - 1);
+        }
+        const TileEntry e = E[s];
+        const unsigned long long below = (1ull << (x.c & (TILE_BITS - 1))) - 1;
+        acc_add<GM>(&acc[e.base + __popcll(e.mask & below)], a * x.v);
+    }
+};
+
+template <class Team>
+__device__ __forceinline__ void build_tiles(const Team& tm, TileEntry* E, bool direct, int lo,
+                                            int H, int hshift, int a0, int a1,
+                                            const int* __restrict__ Acol,
+                                            const int4* __restrict__ bmeta,
+                                            const int* __restrict__ btcol,
+                                            const unsigned long long* __restrict__ btmask,
+                                            int tflop, int4* stage) {
+    const TileBuild f{E, direct, lo, H, hshift, btcol, btmask};
+    for_products(tm, a0, a1, Acol, nullptr, bmeta, true, pick_group(tflop, a1 - a0, Team::size), f,
+                 stage);
+}
+
+template <class Team>
+__device__ __forceinline__ void clear_tiles(const Team& tm, TileEntry* E, int H) {
+    for (int s = tm.rank(); s < H; s += Team::size) {
+        TileEntry z;
+        z.mask = 0;
+        z.base = 0;
+        z.key = -1;
+        E[s] = z;
+    }
+}
+
+// ------------------------------------------------------------- symbolic ---
+struct SymArgs {
+    int M;
+    const int* Aptr;
+    const int* Acol;
+    const int4* bmeta;
+    const int* btcol;
+    const unsigned long long* btmask;
+    const int* rtflop;
+    const int* rlo;
+    const int* rhi;
+    const int* list;
+    const Stats* stats;
+    int bin;
+    int* Cptr;
+    int* ctiles;
+    char* gscratch;
+    long long gbytes;  // per block
+};
+
+template <class Team>
+__device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E, int4* stage) {
+    const int lo = a.rlo[row], hi = a.rhi[row];
+    const int span = hi - lo + 1;
+    const int tflop = a.rtflop[row];
+    const bool direct = sym_direct(span, tflop);
+    const int H = direct ? span : hash_slots(tflop < span ? tflop : span);
+    const int hshift = direct ? 0 : ilog2(H);
+    clear_tiles(tm, E, H);
+    tm.sync();
+    build_tiles(tm, E, direct, lo, H, hshift, a.Aptr[row], a.Aptr[row + 1], a.Acol, a.bmeta,
+                a.btcol, a.btmask, tflop, stage);
+    tm.sync();
+    long long n = 0;
+    int t = 0;
+    for (int s = tm.rank(); s < H; s += Team::size) {
+        const unsigned long long m = E[s].mask;
+        n += __popcll(m);
+        t += m != 0;
+    }
+    n = tm.sum(n);
+    t = tm.sum(t);
+    if (tm.rank() == 0) {
+        a.Cptr[row] = (int)n;
+        a.ctiles[row] = t;
+    }
+    tm.sync();
+}
+
+template <int BYTES>
+__global__ __launch_bounds__(256) void k_sym_wave(SymArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int w = threadIdx.x >> 6;
+    TileEntry* E = (TileEntry*)(smem + w * BYTES + WAVE_HDR);
+    const int count = a.stats->sym_count[a.bin];
+    const int* list = a.list + a.stats->sym_start[a.bin];
+    WaveTeam tm;
+    for (RowWalk rw(count, WPB, w); rw.first < rw.end; rw.first += rw.stride)
+        sym_row(tm, a, list[rw.first], E, nullptr);
+}
+
+template <int T, bool GLOBALMEM>
+__global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    BlockTeam<T, GLOBALMEM> tm{(long long*)smem};
+    TileEntry* E = GLOBALMEM ? (TileEntry*)(a.gscratch + (long long)blockIdx.x * a.gbytes)
+                             : (TileEntry*)(smem + BLOCK_HDR);
+    const int count = a.stats->sym_count[a.bin];
+    const int* list = a.list + a.stats->sym_start[a.bin];
+    int4* stage = (int4*)(smem + 1024);
+    for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
+        sym_row(tm, a, list[rw.first], E, stage);
+}
+
+// ----------------------------------------------------- scan + classify ---
+
+__global__ __launch_bounds__(1024) void k_scan_reduce(int M, const int* __restrict__ Cptr,
+                                                      long long* __restrict__ part) {
+    __shared__ long long ws[16];
+    const int base = blockIdx.x * SCAN_ITEMS;
+    long long s = 0;
+    for (int k = threadIdx.x; k < SCAN_ITEMS; k += 1024) {
+        const int i = base + k;
+        if (i < M) s += Cptr[i];
+    }
+    s = wave_sum(s);
+    if (lane_id() == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (int k = 0; k < 16; ++k) t += ws[k];
+        part[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_scan_top(int nb, long long* __restrict__ part,
+                                                   Stats* __restrict__ stats) {
+    __shared__ long long ws[16];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    long long carry = 0;
+    for (int b = 0; b < nb; b += 1024) {
+        const int i = b + threadIdx.x;
+        const long long x = i < nb ? part[i] : 0;
+        const long long inc = wave_incl_scan64(x);
+        if (lane == 63) ws[w] = inc;
+        __syncthreads();
+        long long woff = 0, tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            const long long v = ws[k];
+            woff += (k < w) ? v : 0;
+            tot += v;
+        }
+        if (i < nb) part[i] = carry + woff + inc - x;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        stats->nnzC = carry;
+        if (carry > INT_MAX) atomicOr(&stats->err, ERR_OVERFLOW);
+    }
+}
+
+__device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed) {
+    if (n == 0) return NUM_NONE;
+    const long long need = num_need(span, t, n);
+    if (need <= NUM_W4_BYTES - WAVE_HDR && flop <= NUM_W4_WORK) return NUM_W4;
+    if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16;
+    if (need <= NUM_B256_BYTES - BLOCK_HDR && flop <= NUM_B256_WORK) return NUM_B256;
+    if (need <= B1024_BYTES) return NUM_B1024;
+    atomicMax(gneed, (int)(need > INT_MAX ? INT_MAX : need));
+    return NUM_GLOBAL;
+}
+
+// Exclusive scan of the C row nnz (items [0, M], item M = 0 gives row_ptr[M])
+// plus the numeric bin of every row.
+__global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cptr,
+                                                     const long long* __restrict__ part,
+                                                     const int* __restrict__ rflop,
+                                                     const int* __restrict__ rlo,
+                                                     const int* __restrict__ rhi,
+                                                     const int* __restrict__ ctiles,
+                                                     unsigned char* __restrict__ bin_id,
+                                                     Stats* __restrict__ stats) {
+    constexpr int PER = SCAN_ITEMS / 1024;
+    __shared__ long long ws[16];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int base = blockIdx.x * SCAN_ITEMS + threadIdx.x * PER;
+    int v[PER];
+    long long loc = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = base + k;
+        v[k] = i < M ? Cptr[i] : 0;
+        loc += v[k];
+    }
+    const long long inc = wave_incl_scan64(loc);
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    long long off = part[blockIdx.x];
+    for (int k = 0; k < w; ++k) off += ws[k];
+    off += inc - loc;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = base + k;
+        if (i <= M) Cptr[i] = (int)off;
+        if (i < M) {
+            const int n = v[k];
+            const int lo = rlo[i], hi = rhi[i];
+            const int span = n ? hi - lo + 1 : 0;
+            bin_id[i] = (unsigned char)num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need);
+        }
+        off += v[k];
+    }
+}
+
+// --------------------------------------------------------------- numeric ---
+struct NumArgs {
+    const int* Aptr;
+    const int* Acol;
+    const double* Aval;
+    const int* Bcol;
+    const double* Bval;
+    const int4* bmeta;
+    const int* btcol;
+    const unsigned long long* btmask;
+    const int* rflop;
+    const int* rtflop;
+    const int* rlo;
+    const int* rhi;
+    const int* ctiles;
+    const int* list;  // already offset to the bin's start
+    int count;
+    const int* Cptr;
+    int* Ccol;
+    double* Cval;
+    char* gscratch;
+    long long gbytes;
+};
+
+template <class Team, bool GLOBALMEM>
+__device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region, int* counter,
+                        int4* stage) {
+    const int lo = a.rlo[row], hi = a.rhi[row];
+    const int span = hi - lo + 1;
+    const int t = a.ctiles[row];
+    const int c0 = a.Cptr[row];
+    const int n = a.Cptr[row + 1] - c0;
+    const bool direct = num_direct(span, t, n);
+    const int H = direct ? span : hash_slots(t);
+    const int hshift = direct ? 0 : ilog2(H);
+    TileEntry* E = (TileEntry*)region;
+    double* acc = (double*)(region + (long long)H * 16);
+    const int a0 = a.Aptr[row], a1 = a.Aptr[row + 1];
+
+    // 1. the C row's tile table (same as the symbolic pass)
+    clear_tiles(tm, E, H);
+    if (!direct && tm.rank() == 0) *counter = 0;
+    tm.sync();
+    build_tiles(tm, E, direct, lo, H, hshift, a0, a1, a.Acol, a.bmeta, a.btcol, a.btmask,
+                a.rtflop[row], stage);
+    tm.sync();
+
+    // 2. rank of every tile's first column = prefix popcount in tile order
+    if (direct) {
+        tm.exclusive_scan(
+            span, [&](int i) { return (int)__popcll(E[i].mask); },
+            [&](int i, int v) { E[i].base = v; });
+    } else {
+        unsigned long long* S = (unsigned long long*)acc;
+        const int P = next_pow2(t);
+        for (int s = tm.rank(); s < H; s += Team::size) {
+            const int key = E[s].key;
+            if (key != -1) {
+                const int idx = atomicAdd(counter, 1);
+                S[idx] = ((unsigned long long)(unsigned)key << 32) | (unsigned)s;
+            }
+        }
+        for (int i = t + tm.rank(); i < P; i += Team::size) S[i] = ~0ull;
+        tm.sync();
+        team_bitonic(tm, S, P);
+        tm.exclusive_scan(
+            t, [&](int e) { return (int)__popcll(E[(int)(unsigned)S[e]].mask); },
+            [&](int e, int v) { E[(int)(unsigned)S[e]].base = v; });
+    }
+    tm.sync();
+    for (int r = tm.rank(); r < n; r += Team::size) acc[r] = 0.0;
+    tm.sync();
+
+    // 3. accumulate: product (c, a*b) -> acc[base(tile) + popc(mask & below(c))]
+    {
+        const Accum<GLOBALMEM> f{E, acc, direct, lo, H, hshift, a.Bcol, a.Bval};
+        for_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false,
+                     pick_group(a.rflop[row], a1 - a0, Team::size), f, stage);
+    }
+    tm.sync();
+
+    // 4. write C: values straight from the accumulator, columns from the tiles
+    for (int r = tm.rank(); r < n; r += Team::size) a.Cval[c0 + r] = acc[r];
+    if (n >= 8 * t) {
+        // dense masks: one wave per tile, lane = bit
+        const int lane = lane_id();
+        const int nw = Team::size / 64, wv = tm.rank() >> 6;
+        for (int s = wv; s < H; s += nw) {
+            const TileEntry e = E[s];
+            const int key = direct ? lo + s : e.key;
+            if (e.mask && ((e.mask >> lane) & 1ull))
+                a.Ccol[c0 + e.base + __popcll(e.mask & lanemask_lt())] = (key << TILE_SHIFT) + lane;
+        }
+    } else {
+        for (int s = tm.rank(); s < H; s += Team::size) {
+            const TileEntry e = E[s];
+            unsigned long long mk = e.mask;
+            if (!mk) continue;
+            const int key = direct ? lo + s : e.key;
+            int r = c0 + e.base;
+            while (mk) {
+                const int b = __builtin_ctzll(mk);
+                a.Ccol[r++] = (key << TILE_SHIFT) + b;
+                mk &= mk - 1;
+            }
+        }
+    }
+    tm.sync();
+}
+
+template <int BYTES>
+__global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int w = threadIdx.x >> 6;
+    char* reg = smem + w * BYTES;
+    WaveTeam tm;
+    for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride)
+        num_row<WaveTeam, false>(tm, a, a.list[rw.first], reg + WAVE_HDR, (int*)reg, nullptr);
+}
+
+template <int T, bool GLOBALMEM>
+__global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    BlockTeam<T, GLOBALMEM> tm{(long long*)smem};
+    char* reg = GLOBALMEM ? (a.gscratch + (long long)blockIdx.x * a.gbytes) : (smem + BLOCK_HDR);
+    int* counter = (int*)(smem + 128);
+    int4* stage = (int4*)(smem + 1024);
+    for (RowWalk rw(a.count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
+        num_row<BlockTeam<T, GLOBALMEM>, GLOBALMEM>(tm, a, a.list[rw.first], reg, counter, stage);
+}
+
+// -------------------------------------------------------------- launchers ---
+
+static int pick_group(long long nnz, int rows) {
+    const long long avg = rows > 0 ? (nnz + rows - 1) / rows : 1;
+    int g = 8;
+    while (g < avg && g < 64) g <<= 1;
+    return g;
+}
+
+static int round8(long long x, int cap) {
+    long long g = x < cap ? x : cap;
+    if (g < 8) g = 8;
+    return (int)((g + 7) / 8 * 8);
+}
+
+void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
+    if (B.M <= 0) return;
+    const int G = pick_group(B.nnz, B.M);
+    const int rpb = 256 / G;
+    const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
+    switch (G) {
+    case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    case 32: hipLaunchKernelGGL(k_mask_b<32>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    default: hipLaunchKernelGGL(k_mask_b<64>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    }
+}
+
+int launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr) {
+    if (A.M <= 0) return 0;
+    const int G = pick_group(A.nnz, A.M);
+    const int rpb = 256 / G;
+    const dim3 grid((A.M + rpb - 1) / rpb), blk(256);
+#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.bin_id, Cptr, w.blkflop, w.stats)
+    switch (G) {
+    case 8: MHS_ANALYZE(8); break;
+    case 16: MHS_ANALYZE(16); break;
+    case 32: MHS_ANALYZE(32); break;
+    default: MHS_ANALYZE(64); break;
+    }
+#undef MHS_ANALYZE
+    return (int)grid.x;
+}
+
+void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks) {
+    if (M <= 0) return;
+    const int nb = phase == 0 ? SYM_NB : NUM_NB;
+    const int nblk = (M + BIN_BLOCK - 1) / BIN_BLOCK;
+    hipLaunchKernelGGL(k_bin_count, dim3(nblk), dim3(BIN_BLOCK), 0, s, M, nb, nblk, w.bin_id, w.blkcnt);
+    int* cnt = phase == 0 ? w.stats->sym_count : w.stats->num_count;
+    long long* st = phase == 0 ? w.stats->sym_start : w.stats->num_start;
+    hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, nb, nblk, w.blkcnt, cnt, st, w.blkflop,
+                       phase == 0 ? nflop_blocks : 0, &w.stats->flop);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(BIN_BLOCK), 0, s, M, nb, nblk, w.bin_id, w.blkcnt, w.rowlist);
+}
+
+void init_kernel_attributes() {
+    // gfx950 grants up to 160 KiB of LDS per workgroup; make the large dynamic
+    // requests explicit for the block-per-row kernels.
+    (void)hipFuncSetAttribute((const void*)k_sym_block<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)k_num_block<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)k_num_block<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+}
+
+size_t sym_global_bytes_per_block(int N) {
+    const int span_max = N > 0 ? ((N - 1) >> TILE_SHIFT) + 1 : 1;
+    return (size_t)hash_slots(span_max) * 16;
+}
+
+void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid) {
+    if (M <= 0) return;
+    SymArgs a;
+    a.M = M;
+    a.Aptr = A.ptr;
+    a.Acol = A.col;
+    a.bmeta = w.bmeta;
+    a.btcol = w.btcol;
+    a.btmask = w.btmask;
+    a.rtflop = w.rtflop;
+    a.rlo = w.rlo;
+    a.rhi = w.rhi;
+    a.list = w.rowlist;
+    a.stats = w.stats;
+    a.Cptr = Cptr;
+    a.ctiles = w.ctiles;
+    a.gscratch = (char*)w.gscratch;
+    a.gbytes = (long long)sym_global_bytes_per_block(N);
+    // Persistent grids: the bin sizes stay on the device (no host round trip);
+    // blocks past a bin's rows exit at once.
+    a.bin = SYM_WAVE;
+    hipLaunchKernelGGL(k_sym_wave<SYM_WAVE_BYTES>, dim3(round8((M + WPB - 1) / WPB, 2048)), dim3(256),
+                       WPB * SYM_WAVE_BYTES, s, a);
+    a.bin = SYM_B256;
+    hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, 1024)), dim3(256), SYM_B256_BYTES, s, a);
+    a.bin = SYM_B1024;
+    hipLaunchKernelGGL((k_sym_block<1024, false>), dim3(round8(M, 256)), dim3(1024), LDS_MAX - 1024, s, a);
+    a.bin = SYM_GLOBAL;
+    hipLaunchKernelGGL((k_sym_block<1024, true>), dim3(global_grid), dim3(1024), BLOCK_HDR, s, a);
+}
+
+void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s) {
+    const int nb = (M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS;
+    long long* part = (long long*)w.scan_part;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(1024), 0, s, M, Cptr, part);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, nb, part, w.stats);
+    hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.rflop, w.rlo, w.rhi,
+                       w.ctiles, w.bin_id, w.stats);
+}
+
+void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
+                    double* Cval, hipStream_t s, int global_grid) {
+    NumArgs a;
+    a.Aptr = A.ptr;
+    a.Acol = A.col;
+    a.Aval = A.val;
+    a.Bcol = B.col;
+    a.Bval = B.val;
+    a.bmeta = w.bmeta;
+    a.btcol = w.btcol;
+    a.btmask = w.btmask;
+    a.rflop = w.rflop;
+    a.rtflop = w.rtflop;
+    a.rlo = w.rlo;
+    a.rhi = w.rhi;
+    a.ctiles = w.ctiles;
+    a.Cptr = Cptr;
+    a.Ccol = Ccol;
+    a.Cval = Cval;
+    a.gscratch = (char*)w.gscratch;
+    a.gbytes = 0;
+    // Largest bins first so the long rows start early.
+    if (h.num_count[NUM_GLOBAL] > 0) {
+        a.list = w.rowlist + h.num_start[NUM_GLOBAL];
+        a.count = h.num_count[NUM_GLOBAL];
+        a.gbytes = align16(h.num_global_need);
+        const int g = a.count < global_grid ? a.count : global_grid;
+        hipLaunchKernelGGL((k_num_block<1024, true>), dim3(g), dim3(1024), BLOCK_HDR, s, a);
+    }
+    if (h.num_count[NUM_B1024] > 0) {
+        a.list = w.rowlist + h.num_start[NUM_B1024];
+        a.count = h.num_count[NUM_B1024];
+        hipLaunchKernelGGL((k_num_block<1024, false>), dim3(round8(a.count, 256)), dim3(1024), LDS_MAX - 1024, s, a);
+    }
+    if (h.num_count[NUM_B256] > 0) {
+        a.list = w.rowlist + h.num_start[NUM_B256];
+        a.count = h.num_count[NUM_B256];
+        hipLaunchKernelGGL((k_num_block<256, false>), dim3(round8(a.count, 1024)), dim3(256), NUM_B256_BYTES, s, a);
+    }
+    if (h.num_count[NUM_W16] > 0) {
+        a.list = w.rowlist + h.num_start[NUM_W16];
+        a.count = h.num_count[NUM_W16];
+        hipLaunchKernelGGL(k_num_wave<NUM_W16_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, 2048)), dim3(256),
+                           WPB * NUM_W16_BYTES, s, a);
+    }
+    if (h.num_count[NUM_W4] > 0) {
+        a.list = w.rowlist + h.num_start[NUM_W4];
+        a.count = h.num_count[NUM_W4];
+        hipLaunchKernelGGL(k_num_wave<NUM_W4_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, 4096)), dim3(256),
+                           WPB * NUM_W4_BYTES, s, a);
+    }
+}
+
+}  // namespace mhs

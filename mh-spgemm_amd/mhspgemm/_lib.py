@@ -1,0 +1,104 @@
+"""ctypes binding of libmhspgemm.so (the C-ABI declared in include/mhspgemm.h).
+
+The shared library is built in-tree (``make -C mh-spgemm_amd``) and loaded from
+this directory.  There is no fallback: if the library is missing, importing the
+package raises, so no caller can silently run anything but the HIP path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "libmhspgemm.so"
+HEADER = HERE.parent.parent / "include" / "mhspgemm.h"
+
+MHS_OK = 0
+MHS_ERR_HIP = 1
+MHS_ERR_OOM = 2
+MHS_ERR_INVALID = 3
+MHS_ERR_OVERFLOW = 4
+MHS_ERR_IO = 5
+
+STATUS_NAMES = {0: "MHS_OK", 1: "MHS_ERR_HIP", 2: "MHS_ERR_OOM", 3: "MHS_ERR_INVALID",
+                4: "MHS_ERR_OVERFLOW", 5: "MHS_ERR_IO"}
+
+
+class mhs_csr(ctypes.Structure):
+    _fields_ = [("M", ctypes.c_int32), ("N", ctypes.c_int32), ("nnz", ctypes.c_int32),
+                ("ptr", ctypes.c_void_p), ("col", ctypes.c_void_p), ("val", ctypes.c_void_p)]
+
+
+class mhs_timing(ctypes.Structure):
+    _fields_ = [("mem_alloc", ctypes.c_double), ("Form_mask_matrix_B", ctypes.c_double),
+                ("symbolic_binning", ctypes.c_double), ("Calculate_C_nnz", ctypes.c_double),
+                ("numeric_binning", ctypes.c_double), ("Malloc_C_col_val", ctypes.c_double),
+                ("Numeric", ctypes.c_double), ("total_ref", ctypes.c_double),
+                ("total_e2e", ctypes.c_double), ("flop", ctypes.c_uint64), ("nnzC", ctypes.c_int64),
+                ("sym_bins", ctypes.c_int32 * 8), ("num_bins", ctypes.c_int32 * 8)]
+
+
+class mhs_host_csr(ctypes.Structure):
+    _fields_ = [("M", ctypes.c_int32), ("N", ctypes.c_int32), ("nnz", ctypes.c_int32),
+                ("ptr", ctypes.c_void_p), ("col", ctypes.c_void_p), ("val", ctypes.c_void_p),
+                ("is_symmetric", ctypes.c_int32)]
+
+
+def declared_functions() -> list[str]:
+    """Names of the functions include/mhspgemm.h declares."""
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mhs_[a-z0-9_]+)\s*\(", text)))
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()' or make -C mh-spgemm_amd)")
+    L = ctypes.CDLL(str(LIB_PATH))
+    c_int, c_void_p, c_size_t = ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
+    P = ctypes.POINTER
+    L.mhs_abi_version.restype = c_int
+    L.mhs_ctx_create.argtypes = [P(c_void_p), c_int]
+    L.mhs_ctx_create.restype = c_int
+    L.mhs_ctx_destroy.argtypes = [c_void_p]
+    L.mhs_ctx_destroy.restype = None
+    L.mhs_last_error.argtypes = [c_void_p]
+    L.mhs_last_error.restype = ctypes.c_char_p
+    L.mhs_ctx_set_stream.argtypes = [c_void_p, c_void_p]
+    L.mhs_ctx_set_stream.restype = c_int
+    L.mhs_ctx_trim.argtypes = [c_void_p]
+    L.mhs_ctx_trim.restype = c_int
+    L.mhs_spgemm.argtypes = [c_void_p, P(mhs_csr), P(mhs_csr), P(mhs_csr), P(mhs_timing)]
+    L.mhs_spgemm.restype = c_int
+    L.mhs_csr_free.argtypes = [P(mhs_csr)]
+    L.mhs_csr_free.restype = None
+    L.mhs_ctx_recycle.argtypes = [c_void_p, P(mhs_csr)]
+    L.mhs_ctx_recycle.restype = None
+    L.mhs_read_mtx.argtypes = [ctypes.c_char_p, P(mhs_host_csr)]
+    L.mhs_read_mtx.restype = c_int
+    L.mhs_host_csr_free.argtypes = [P(mhs_host_csr)]
+    L.mhs_host_csr_free.restype = None
+    L.mhs_flop_count.argtypes = [ctypes.c_int32, c_void_p, c_void_p]
+    L.mhs_flop_count.restype = ctypes.c_uint64
+    L.mhs_memcpy.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int]
+    L.mhs_memcpy.restype = c_int
+    L.mhs_device_alloc.argtypes = [c_void_p, P(c_void_p), c_size_t]
+    L.mhs_device_alloc.restype = c_int
+    L.mhs_device_free.argtypes = [c_void_p, c_void_p]
+    L.mhs_device_free.restype = c_int
+    _lib = L
+    return L
+
+
+def lib_path() -> str:
+    return os.fspath(LIB_PATH)

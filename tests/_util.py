@@ -1,0 +1,96 @@
+"""Shared test helpers (test infrastructure)."""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def load_golden(name: str):
+    d = json.loads((GOLDEN / f"{name}.json").read_text())
+    ptr = np.asarray(d["ptr"], np.int32)
+    col = np.asarray(d["col"], np.int32)
+    val = np.asarray([float.fromhex(x) for x in d["val_hex"]], np.float64)
+    return d, ptr, col, val
+
+
+PRODUCT_CASES = ["cage4_like", "tile_edges", "dense_row_col", "duplicates", "rect_AB", "empty_product"]
+READ_CASES = ["mm_symmetric", "mm_skew", "mm_hermitian", "mm_pattern", "mm_integer", "mm_dups_comments"]
+
+
+def csr_from_arrays(M, N, ptr, col, val):
+    import mhspgemm
+    return mhspgemm.CSR(M, N, ptr, col, val)
+
+
+def random_csr(M, N, per_row, seed, lo=0.1, hi=1.0, sorted_unique=True, signed=False):
+    rng = np.random.default_rng(seed)
+    lens = rng.poisson(per_row, M)
+    rows = np.repeat(np.arange(M), lens)
+    cols = rng.integers(0, N, len(rows))
+    key = np.unique(rows.astype(np.int64) * N + cols) if sorted_unique else rows.astype(np.int64) * N + cols
+    r = key // N
+    c = (key % N).astype(np.int32)
+    ptr = np.zeros(M + 1, np.int64)
+    np.cumsum(np.bincount(r, minlength=M), out=ptr[1:])
+    v = rng.uniform(lo, hi, len(c))
+    if signed:
+        v *= rng.choice([-1.0, 1.0], len(c))
+    return ptr.astype(np.int32), c, v
+
+
+def bin_zoo(seed: int = 11):
+    """A (rows of every kind) x B (K x N, N = 2M columns) such that rows land in
+    every symbolic and numeric bin, including both global-memory fallbacks:
+    empty, single product, banded (direct tables), scattered (hashed tables)
+    of growing size, heavy work on a tiny pattern (duplicate A entries)."""
+    rng = np.random.default_rng(seed)
+    N = 2_000_000
+    K = 3000
+    # B rows: 0..999 "band" (64 consecutive cols), 1000..2999 "scatter" (50 random cols), row 2999 single entry
+    Brows, Bcols = [], []
+    for k in range(K):
+        if k == K - 1:
+            cs = np.array([12345])
+        elif k < 1000:
+            off = 1000 * k % (N - 64)
+            cs = np.arange(off, off + 64)
+        else:
+            cs = np.unique(rng.integers(0, N, 50))
+        Brows.append(np.full(len(cs), k))
+        Bcols.append(cs)
+    Br = np.concatenate(Brows)
+    Bc = np.concatenate(Bcols)
+    Bkey = Br.astype(np.int64) * N + Bc
+    order = np.argsort(Bkey, kind="stable")
+    Br, Bc = Br[order], Bc[order]
+    Bptr = np.zeros(K + 1, np.int64)
+    np.cumsum(np.bincount(Br, minlength=K), out=Bptr[1:])
+    Bv = rng.uniform(0.1, 1.0, len(Bc))
+
+    arows = []  # list of lists of k (A entries, in order, duplicates allowed)
+    arows.append([])                                 # empty
+    arows.append([K - 1])                            # single product
+    for i in range(20):                              # banded, small: direct, wave
+        s = int(rng.integers(0, 990))
+        arows.append(list(range(s, s + 8)))
+    for i in range(10):                              # scattered small: hash, wave
+        arows.append(sorted(rng.choice(np.arange(1000, K - 1), 2, replace=False).tolist()))
+    for i in range(6):                               # scattered medium: hash, 256-thread block
+        arows.append(sorted(rng.choice(np.arange(1000, K - 1), 20, replace=False).tolist()))
+    for i in range(4):                               # scattered large: 1024-thread block
+        arows.append(sorted(rng.choice(np.arange(1000, K - 1), 60, replace=False).tolist()))
+    for i in range(2):                               # scattered huge: global memory
+        arows.append(sorted(rng.choice(np.arange(1000, K - 1), 400, replace=False).tolist()))
+    arows.append([5] * 3000)                         # heavy work, tiny pattern (duplicates)
+    arows.append(sorted(rng.choice(np.arange(0, 1000), 200, replace=False).tolist()))  # wide banded
+    arows.append(list(range(0, 1000, 3)))            # direct, large span
+    M = len(arows)
+    Aptr = np.zeros(M + 1, np.int64)
+    Aptr[1:] = np.cumsum([len(r) for r in arows])
+    Acol = np.array([k for r in arows for k in r], np.int32)
+    Av = rng.uniform(0.1, 1.0, len(Acol))
+    return (M, K, Aptr.astype(np.int32), Acol, Av), (K, N, Bptr.astype(np.int32), Bc.astype(np.int32), Bv)

@@ -1,0 +1,216 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle.
+
+Bar (BASELINE.json north_star): row_ptr and col_idx bit-exact; values within
+1e-6 relative (|d| <= 1e-6*|ref| or |d| <= 1e-12), with the reference's own
+1e-9 rule (src/CSR.cu:79-80) also checked where values are positive.  With
+mixed-sign values (cancellation) the value tolerance is 1e-6 of the sum of
+|a*b| of the entry, the pattern stays exact (structural zeros are kept).
+"""
+import numpy as np
+import pytest
+
+import mhspgemm
+from mhspgemm import synth
+from oracle import oracle as orc
+from _util import GOLDEN, PRODUCT_CASES, bin_zoo, load_golden, random_csr
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 1e-6, 1e-12
+
+
+def run_gpu(tool, A, B):
+    A.H2D(tool.device)
+    if B is not A:
+        B.H2D(tool.device)
+    C, t = mhspgemm.spgemm(tool, A, B)
+    try:
+        p, c, v = C.to_host()
+    finally:
+        C.release()
+    return p, c, v, t
+
+
+def check(tool, A, B, ref_rule=True):
+    p, c, v, t = run_gpu(tool, A, B)
+    Cp, Ci, Cv = orc.spgemm(A.ptr, A.col, A.val, B.ptr, B.col, B.val, B.N)
+    assert np.array_equal(p, Cp), "row_ptr must be bit-exact"
+    assert np.array_equal(c, Ci), "col_idx must be bit-exact"
+    ok, *_ = mhspgemm.compare_tol(Cp, Ci, Cv, p, c, v, RTOL, ATOL)
+    assert ok, "values outside 1e-6 relative"
+    if ref_rule:
+        assert orc.compare_ref(Cp, Ci, Cv, p, c, v) == 1, "reference 1e-9 rule"
+    assert t.nnzC == Cp[-1]
+    assert t.flop == orc.flop(A.col, B.ptr)
+    return t
+
+
+@pytest.mark.parametrize("name", PRODUCT_CASES)
+def test_golden_products(tool, name):
+    d, gp, gc, gv = load_golden(name)
+    A = mhspgemm.CSR()
+    assert mhspgemm.readMtxFile(A, str(GOLDEN / d["A"])) == 0
+    if d["B"]:
+        B = mhspgemm.CSR()
+        assert mhspgemm.readMtxFile(B, str(GOLDEN / d["B"])) == 0
+    else:
+        B = A
+    p, c, v, t = run_gpu(tool, A, B)
+    assert np.array_equal(p, gp) and np.array_equal(c, gc)
+    ok, *_ = mhspgemm.compare_tol(gp, gc, gv, p, c, v, RTOL, ATOL)
+    assert ok
+
+
+def test_cage4_like(tool):
+    A = synth.cage4_like()
+    check(tool, A, A)
+
+
+def test_cant_like_full(tool):
+    A = synth.cant_like()
+    t = check(tool, A, A)
+    assert t.flop > 3e8
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_rect(tool, seed):
+    p, c, v = random_csr(3000, 2000, 7, seed)
+    Bp, Bc, Bv = random_csr(2000, 50_000, 12, seed + 100)
+    A = mhspgemm.CSR(3000, 2000, p, c, v)
+    B = mhspgemm.CSR(2000, 50_000, Bp, Bc, Bv)
+    check(tool, A, B)
+
+
+def test_bin_zoo_every_bin(tool):
+    (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = bin_zoo()
+    A = mhspgemm.CSR(M, K, Ap, Ac, Av)
+    B = mhspgemm.CSR(K2, N, Bp, Bc, Bv)
+    t = check(tool, A, B)
+    # every symbolic bin (1..4) and numeric bin (1..5) saw rows
+    assert all(t.sym_bins[i] > 0 for i in range(0, 5)), t.sym_bins
+    assert all(t.num_bins[i] > 0 for i in range(0, 6)), t.num_bins
+
+
+def test_mixed_sign_cancellation_keeps_structure(tool):
+    p, c, v = random_csr(1500, 1500, 10, seed=9, signed=True)
+    A = mhspgemm.CSR(1500, 1500, p, c, v)
+    gp, gc, gv, _ = run_gpu(tool, A, A)
+    Cp, Ci, Cv = orc.spgemm(p, c, v, p, c, v, 1500)
+    assert np.array_equal(gp, Cp) and np.array_equal(gc, Ci)
+    # tolerance scaled by sum |a*b| per entry
+    _, _, absv = orc.spgemm(p, c, np.abs(v), p, c, np.abs(v), 1500)
+    assert np.all(np.abs(gv - Cv) <= 1e-6 * absv + 1e-300)
+
+
+def test_exact_cancellation_structural_zero(tool):
+    p = np.array([0, 2, 4], np.int32)
+    c = np.array([0, 1, 0, 1], np.int32)
+    v = np.array([1.0, 1.0, 1.0, -1.0])
+    A = mhspgemm.CSR(2, 2, p, c, v)
+    gp, gc, gv, _ = run_gpu(tool, A, A)
+    assert gp.tolist() == [0, 2, 4] and gc.tolist() == [0, 1, 0, 1]
+    assert gv.tolist() == [2.0, 0.0, 0.0, 2.0]
+
+
+def test_empty_and_degenerate(tool):
+    # all-empty rows
+    A = mhspgemm.CSR(5, 5, np.zeros(6, np.int32), np.zeros(0, np.int32), np.zeros(0))
+    p, c, v, t = run_gpu(tool, A, A)
+    assert p.tolist() == [0] * 6 and len(c) == 0
+    # 1x1
+    A = mhspgemm.CSR(1, 1, np.array([0, 1], np.int32), np.array([0], np.int32), np.array([3.0]))
+    p, c, v, t = run_gpu(tool, A, A)
+    assert p.tolist() == [0, 1] and c.tolist() == [0] and v.tolist() == [9.0]
+
+
+def test_error_unsorted_B(tool):
+    p = np.array([0, 2, 3], np.int32)
+    c = np.array([1, 0, 1], np.int32)  # row 0 unsorted
+    A = mhspgemm.CSR(2, 2, p, c, np.ones(3))
+    A.H2D(tool.device)
+    with pytest.raises(mhspgemm.MHSpGEMMError) as e:
+        mhspgemm.spgemm(tool, A, A)
+    assert e.value.status == 3 and "sorted" in str(e.value)
+
+
+def test_error_dimension_mismatch(tool):
+    A = mhspgemm.CSR(2, 3, np.array([0, 1, 2], np.int32), np.array([0, 2], np.int32), np.ones(2))
+    A.H2D(tool.device)
+    with pytest.raises(mhspgemm.MHSpGEMMError) as e:
+        mhspgemm.spgemm(tool, A, A)
+    assert e.value.status == 3
+
+
+def test_error_column_out_of_range(tool):
+    A = mhspgemm.CSR(2, 2, np.array([0, 1, 2], np.int32), np.array([0, 5], np.int32), np.ones(2))
+    A.H2D(tool.device)
+    with pytest.raises(mhspgemm.MHSpGEMMError):
+        mhspgemm.spgemm(tool, A, A)
+
+
+def test_repeat_calls_reuse_workspace(tool):
+    A = synth.cage4_like()
+    A.H2D(tool.device)
+    ref = None
+    for _ in range(5):
+        C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
+        got = C.to_host()
+        C.release()
+        if ref is None:
+            ref = got
+        assert all(np.array_equal(x, y) for x, y in zip(ref[:2], got[:2]))
+
+
+def test_mirror_interface_MH_spgemm(tool):
+    A = synth.cage4_like()
+    B = A
+    A.H2D(tool.device)
+    C = mhspgemm.CSR()
+    timing = mhspgemm.Timing()
+    mhspgemm.MH_spgemm(A, B, C, timing, tool)
+    C.D2H()
+    Cp, Ci, Cv = orc.spgemm(A.ptr, A.col, A.val, A.ptr, A.col, A.val, A.N)
+    ref = mhspgemm.CSR(A.M, A.N, Cp, Ci, Cv)
+    assert C == ref
+    assert timing.getTotal() > 0 and timing.flop == orc.flop(A.col, A.ptr)
+    C.d_release_csr()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["webbase-1M", "mac_econ_fwd500", "scircuit", "cop20k_A"])
+def test_baseline_configs_full(tool, name):
+    A = synth.SYNTH[name]()
+    check(tool, A, A)
+
+
+@pytest.mark.slow
+def test_cage15_like_rowsample_and_checksum(tool):
+    """Full-size cage15-like: rows sampled against the oracle bit-exactly in
+    pattern; whole-matrix checksum C*1 == A*(B*1) (linearity)."""
+    A = synth.cage15_like()
+    A.H2D(tool.device)
+    C, t = mhspgemm.spgemm(tool, A, A)
+    p, c, v = C.to_host()
+    C.release()
+    assert t.flop == orc.flop(A.col, A.ptr)
+    rng = np.random.default_rng(0)
+    rows = np.sort(rng.choice(A.M, 20000, replace=False))
+    # sub-A = the sampled rows of A
+    lens = np.diff(A.ptr)[rows]
+    sp = np.zeros(len(rows) + 1, np.int64)
+    sp[1:] = np.cumsum(lens)
+    idx = np.concatenate([np.arange(A.ptr[r], A.ptr[r + 1]) for r in rows])
+    Sp, Sc, Sv = sp.astype(np.int32), A.col[idx], A.val[idx]
+    Cp, Ci, Cv = orc.spgemm(Sp, Sc, Sv, A.ptr, A.col, A.val, A.N)
+    for k, r in enumerate(rows):
+        a, b = p[r], p[r + 1]
+        assert b - a == Cp[k + 1] - Cp[k]
+        assert np.array_equal(c[a:b], Ci[Cp[k]:Cp[k + 1]])
+        assert np.allclose(v[a:b], Cv[Cp[k]:Cp[k + 1]], rtol=RTOL, atol=ATOL)
+    # linearity: C*1 = A*(A*1)
+    ones = np.ones(A.N)
+    import scipy.sparse as sps
+    S = sps.csr_matrix((A.val, A.col, A.ptr), shape=(A.M, A.N))
+    lhs = np.bincount(np.repeat(np.arange(A.M), np.diff(p)), weights=v, minlength=A.M)
+    rhs = S @ (S @ ones)
+    assert np.allclose(lhs, rhs, rtol=1e-9)
