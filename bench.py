@@ -1,0 +1,251 @@
+"""bench.py -- GFLOPS of C = A*A (CSR, FP64) on MI355X, the BASELINE.json metric.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--matrix NAME] [--no-cpu]
+
+Workload (BASELINE.json configs[1]): cant.mtx A*A.  The real file is read from
+$MHS_MATRIX_DIR/cant/cant.mtx when present; otherwise the synthetic cant-like
+stand-in (mhspgemm.synth.cant_like: 62,451 rows, 27-point FEM stencil x 3 dof,
+nnz(A*A) 17.5M vs the real 17.4M).  A "step" is one full SpGEMM: device-
+resident A -> device-resident sorted C (mask formation, symbolic, numeric, C
+allocation included: the t_e2e of BASELINE.md §2), C handed back to the
+context's output pool after the step.
+
+N = 1: one process.  N > 1 (torchrun, one rank per GPU, RCCL): rows of A are
+partitioned by flop, each rank starts with its row block of A (= of B), and a
+step is allgatherv(B) over xGMI + the local SpGEMM; C stays distributed (the
+gathered variant is reported beside it).  Total work is fixed, so scaling is
+"strong".
+
+One JSON line on rank 0: value = 2*flop / (max over ranks of the time per step).
+  roofline: the dominant kernel (the numeric phase: k_num_wave for this
+            workload), achieved = algorithmic bytes per launch (BASELINE.md §2:
+            B_alg = 8(M+1) + 20 nnz(A) + 12 flop + 12 nnz(C)) / its average
+            duration from hipEvents recorded on the launch stream during the
+            timed steps; traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per launch
+            from the committed PMC pass (profiles/), else null.
+  cpu_baseline: the oracle (CPU restatement, "port") on the same matrix, all
+            host cores, median of repeats.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for p in (str(ROOT), str(ROOT / "mh-spgemm_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def b_alg(M, nnzA, flop, nnzC):
+    return 8 * (M + 1) + 20 * nnzA + 12 * flop + 12 * nnzC
+
+
+def pmc_traffic(kernel_prefix: str):
+    """Per-launch HBM bytes of the kernel from the committed rocprofv3 PMC
+    summary (FETCH_SIZE doubled per the gfx950 correction, + WRITE_SIZE)."""
+    f = ROOT / "profiles" / "pmc_summary.json"
+    if not f.exists():
+        return None, None
+    try:
+        d = json.loads(f.read_text())
+        k = d.get("kernels", {}).get(kernel_prefix)
+        if not k:
+            return None, None
+        return float(k["hbm_bytes_per_launch"]), d.get("source")
+    except Exception:
+        return None, None
+
+
+def cpu_baseline(A, budget_s: float = 12.0):
+    """Oracle (C restatement of the reference path) on the same workload,
+    every host core; repeats until ~budget_s of CPU work, median."""
+    from oracle import oracle as orc
+    threads = orc.max_threads()
+    times = []
+    t_start = time.time()
+    while True:
+        t0 = time.perf_counter()
+        orc.spgemm(A.ptr, A.col, A.val, A.ptr, A.col, A.val, A.N, nthreads=threads)
+        times.append(time.perf_counter() - t0)
+        if time.time() - t_start > budget_s or len(times) >= 50:
+            break
+    t1 = []  # one-thread figure, a single run
+    t0 = time.perf_counter()
+    orc.spgemm(A.ptr, A.col, A.val, A.ptr, A.col, A.val, A.N, nthreads=1)
+    t1.append(time.perf_counter() - t0)
+    return float(np.median(times)), threads, len(times), t1[0]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--matrix", default="cant")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--gather", action="store_true", help="N>1: also time the gatherv of C to rank 0")
+    args = ap.parse_args()
+
+    import torch
+    import mhspgemm
+    from mhspgemm import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    N_GPUS = world
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    A, source = synth.load_or_synth(args.matrix)
+    flop = mhspgemm.flop_count_np(A.col, A.ptr)
+    tool = mhspgemm.Tool(local)
+    tool.set_stream(torch.cuda.current_stream(local).cuda_stream)
+    dev = f"cuda:{local}"
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(local)
+
+    numeric_ms = []
+    phases = []
+    nnzC = 0
+    gather_ms = None
+    if world == 1:
+        A.H2D(local)
+        for _ in range(args.warmup):
+            C, t = mhspgemm.spgemm(tool, A, A, timing=True)
+            nnzC = C.nnz
+            C.release()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            C, t = mhspgemm.spgemm(tool, A, A, timing=True)
+            numeric_ms.append(t.Numeric)
+            phases.append(t)
+            C.release()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        t_max = elapsed
+        nnzC = t.nnzC
+    else:
+        from mhspgemm import distributed as D
+        rf = D.row_flop(A.ptr, A.col, A.ptr)
+        bnd = D.partition_rows(rf, world)
+        blk = D.local_block(A.ptr, A.col, A.val, int(bnd[rank]), int(bnd[rank + 1]), dev)
+        mult = D.hip_local_multiply(tool)
+        for _ in range(args.warmup):
+            C, _ = D.spgemm_rowsharded(blk, A.N, mult)
+            C.release()
+        barrier()
+        t0 = time.perf_counter()
+        nloc = 0
+        for _ in range(args.steps):
+            C, _ = D.spgemm_rowsharded(blk, A.N, mult)
+            nloc = C.nnz
+            C.release()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+        nn = torch.tensor([nloc], dtype=torch.int64, device=dev)
+        dist.all_reduce(nn)
+        nnzC = int(nn.item())
+        if args.gather:
+            C, _ = D.spgemm_rowsharded(blk, A.N, mult)
+            barrier()
+            g0 = time.perf_counter()
+            D.gather_result(C, blk)
+            barrier()
+            gather_ms = (time.perf_counter() - g0) * 1e3
+            C.release()
+
+    ms_per_step = t_max / args.steps * 1e3
+    gflops = 2.0 * flop / (ms_per_step * 1e-3) / 1e9
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    balg = b_alg(A.M, A.nnz, flop, nnzC)
+    out = {
+        "metric": METRIC,
+        "value": round(gflops, 2),
+        "unit": "GFLOPS",
+        "n_gpus": N_GPUS,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic" if source.startswith("synthetic") else "file",
+        "config": {
+            "workload": f"{args.matrix}.mtx A*A ({source}), device-resident A -> device-resident sorted C",
+            "matrix": args.matrix, "rows": A.M, "nnzA": A.nnz, "flop": flop, "nnzC": nnzC,
+            "parallelism": "single GPU" if N_GPUS == 1 else f"row-sharded x{N_GPUS}, allgatherv(B) in step, C distributed",
+        },
+        "e2e_alg_GBps": round(balg / (ms_per_step * 1e-3) / 1e9, 1),
+    }
+    if N_GPUS == 1:
+        avg_num = float(np.mean(numeric_ms))
+        achieved = balg / (avg_num * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic("k_num_wave")
+        out["roofline"] = {
+            "bound": "hbm", "kernel": "numeric phase (k_num_wave<4096> for this workload)",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic, "traffic_source": tsrc,
+            "alg_bytes_per_launch": balg, "avg_launch_ms": round(avg_num, 4),
+        }
+        ph = {k: round(float(np.mean([getattr(p, k) for p in phases])), 4)
+              for k in ("mem_alloc", "Form_mask_matrix_B", "symbolic_binning", "Calculate_C_nnz",
+                        "numeric_binning", "Malloc_C_col_val", "Numeric", "total_e2e")}
+        ph["t_ref_getTotal"] = round(float(np.mean([p.getTotal() for p in phases])), 4)
+        out["phases_ms"] = ph
+        out["bins"] = {"symbolic": phases[-1].sym_bins[:5], "numeric": phases[-1].num_bins[:6]}
+        if not args.no_cpu:
+            med, threads, reps, one = cpu_baseline(A)
+            out["cpu_baseline"] = {
+                "value": round(2.0 * flop / med / 1e9, 3), "unit": "GFLOPS", "cores": threads,
+                "kind": "port",
+                "sample": f"full {args.matrix} A*A (symbolic+numeric, Gustavson, oracle/), median of {reps} "
+                          f"runs of {med*1e3:.1f} ms on {threads} threads; 1 thread: "
+                          f"{2.0 * flop / one / 1e9:.3f} GFLOPS ({one*1e3:.0f} ms)",
+            }
+        else:
+            out["cpu_baseline"] = None
+    else:
+        out["roofline"] = None
+        out["cpu_baseline"] = None
+        if gather_ms is not None:
+            out["gather_C_ms"] = round(gather_ms, 3)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

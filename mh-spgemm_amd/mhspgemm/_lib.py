@@ -64,6 +64,15 @@ def lib() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()' or make -C mh-spgemm_amd)")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 /
+    # libhsa-runtime64 (same SONAMEs as /opt/rocm's).  Loading torch first makes
+    # the dynamic loader bind our NEEDED libamdhip64.so.7 to the copy already in
+    # the process; the other order maps two HSA runtimes and the second one
+    # finds no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(str(LIB_PATH))
     c_int, c_void_p, c_size_t = ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
     P = ctypes.POINTER
