@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -35,6 +36,7 @@ struct mhs_ctx {
     size_t gscratch_bytes = 0;
     Stats* h_stats = nullptr;  // pinned
     hipEvent_t ev[8] = {};
+    int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays)
     std::vector<std::pair<void*, size_t>> pool;
     std::unordered_map<void*, size_t> sizes;
@@ -190,6 +192,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
         return e == hipErrorOutOfMemory ? MHS_ERR_OOM : MHS_ERR_HIP;
     }
     ctx->stream = ctx->own_stream;
+    if (const char* e = getenv("MHS_DENSE_SPAN")) ctx->dense_span_max = atoi(e);
     init_kernel_attributes();
     *out = ctx;
     return MHS_OK;
@@ -319,7 +322,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
     if (M > 0) {
-        launch_scan_classify(M, w, out.ptr, s);
+        launch_scan_classify(M, w, out.ptr, s, ctx->dense_span_max);
         launch_binning(M, w, 1, s, 0);
     }
     MHS_HIP(hipGetLastError());
@@ -364,7 +367,8 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
 
     // ---- Numeric -------------------------------------------------------------------------
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
-    if (out.nnz > 0) launch_numeric(a, b, w, h, out.ptr, out.col, out.val, s, NUM_GLOBAL_GRID);
+    if (out.nnz > 0)
+        launch_numeric(a, b, w, h, out.ptr, out.col, out.val, s, NUM_GLOBAL_GRID, ctx->dense_span_max);
     MHS_HIP(hipGetLastError());
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[6], s));
     MHS_HIP(hipStreamSynchronize(s));

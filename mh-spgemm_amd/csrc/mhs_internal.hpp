@@ -105,19 +105,31 @@ __host__ __device__ inline long long sym_need(int span, int tflop) {
     int e = sym_direct(span, tflop) ? span : hash_slots(bound);
     return (long long)e * 16;
 }
-// Numeric: tile table (direct or hash) + accumulator / sort region.
-__host__ __device__ inline bool num_direct(int span, int t, int n) {
-    long long nd = (long long)span * 16 + align16((long long)n * 8);
-    int h = hash_slots(t);
-    int p = next_pow2(t);
-    long long nh = (long long)h * 16 + align16((long long)(n > p ? n : p) * 8);
-    return nd <= nh;
+// Numeric row modes:
+//   NM_DENSE  narrow tile span: a dense accumulator over the span's columns
+//             (span*64 doubles) -- a product is one ds_add_f64 at (col - base),
+//             the rank compaction happens once per C entry at output time;
+//   NM_DIRECT tile table direct-mapped over the span + rank-compressed accumulator
+//             (n doubles): a product lands at base(tile) + popc(mask & below(col));
+//   NM_HASH   scattered rows: hashed tile table + rank-compressed accumulator
+//             (tiles sorted by key to assign bases).
+enum NumMode : int { NM_DENSE = 0, NM_DIRECT = 1, NM_HASH = 2 };
+__host__ __device__ inline long long num_need_dense(int span) { return (long long)span * (16 + 64 * 8); }
+__host__ __device__ inline long long num_need_direct(int span, int n) {
+    return (long long)span * 16 + align16((long long)n * 8);
 }
-__host__ __device__ inline long long num_need(int span, int t, int n) {
-    if (num_direct(span, t, n)) return (long long)span * 16 + align16((long long)n * 8);
-    int h = hash_slots(t);
-    int p = next_pow2(t);
+__host__ __device__ inline long long num_need_hash(int t, int n) {
+    const int h = hash_slots(t);
+    const int p = next_pow2(t);
     return (long long)h * 16 + align16((long long)(n > p ? n : p) * 8);
+}
+__host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_max) {
+    if (span <= dense_span_max) return NM_DENSE;
+    return num_need_direct(span, n) <= num_need_hash(t, n) ? NM_DIRECT : NM_HASH;
+}
+__host__ __device__ inline long long num_need(int span, int t, int n, int dense_span_max) {
+    const int m = num_mode(span, t, n, dense_span_max);
+    return m == NM_DENSE ? num_need_dense(span) : m == NM_DIRECT ? num_need_direct(span, n) : num_need_hash(t, n);
 }
 
 // ------------------------------------------------------------ launchers ---
@@ -155,9 +167,9 @@ int launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr
 void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks);  // phase 0 sym, 1 num
 void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s,
                      int global_grid);
-void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s);
+void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max);
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
-                    int* Ccol, double* Cval, hipStream_t s, int global_grid);
+                    int* Ccol, double* Cval, hipStream_t s, int global_grid, int dense_span_max);
 size_t sym_global_bytes_per_block(int N);
 void init_kernel_attributes();
 

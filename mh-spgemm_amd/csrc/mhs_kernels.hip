@@ -29,6 +29,32 @@
 
 #include <climits>
 
+#ifndef MHS_NUM_DIAG
+#define MHS_NUM_DIAG 0  // != 0 only in tools/diag timing builds (wrong results by design)
+#endif
+#ifndef MHS_UNROLL
+#define MHS_UNROLL 4  // B entries per lane issued together in the product walk
+#endif
+#ifndef MHS_BLOCKDIST
+#define MHS_BLOCKDIST 1  // A entries -> lane groups: 1 block distribution, 0 cyclic
+#endif
+#if MHS_NUM_DIAG == 9  // diagnostic build: per-phase s_memtime cycles of the numeric rows
+__device__ unsigned long long g_diag[8];
+#define MHS_STAMP0() unsigned long long tp_ = __builtin_amdgcn_s_memtime()
+#define MHS_STAMP(k)                                                    \
+    do {                                                                \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+        if (tm.rank() == 0) atomicAdd(&g_diag[k], t_ - tp_);           \
+        tp_ = t_;                                                       \
+    } while (0)
+extern "C" int mhs_diag_read(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(g_diag));
+}
+#else
+#define MHS_STAMP0()
+#define MHS_STAMP(k)
+#endif
+
 namespace mhs {
 
 // ------------------------------------------------------------------ helpers ---
@@ -473,14 +499,16 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(int M, int nb, int nb
 
 template <class F>
 __device__ __forceinline__ void run_segment(const F& f, int s, int n, int gl, int G, double a) {
+    constexpr int U = MHS_UNROLL;
     int q = gl;
-    for (; q + G < n; q += 2 * G) {
-        const auto x = f.load(s + q);
-        const auto y = f.load(s + q + G);
-        f.put(x, a);
-        f.put(y, a);
+    for (; q + (U - 1) * G < n; q += U * G) {
+        typename F::Item x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = f.load(s + q + u * G);
+#pragma unroll
+        for (int u = 0; u < U; ++u) f.put(x[u], a);
     }
-    if (q < n) f.put(f.load(s + q), a);
+    for (; q < n; q += G) f.put(f.load(s + q), a);
 }
 
 template <class F>
@@ -505,10 +533,14 @@ __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
         const int nloc = min(64, a1 - jb);
         const int iters = (nloc + ngrp - 1) / ngrp;
         for (int it = 0; it < iters; ++it) {
-            const int e = it * ngrp + grp;  // all lanes active at the shuffles
-            const int s = __shfl(st, e);
-            const int n = __shfl(ln, e);    // 0 for e >= nloc (lane e had no entry)
-            const double a = __shfl(av, e);
+            // block distribution: groups run A entries far apart in the row at the same
+            // time (consecutive entries -- e.g. the dofs of one FEM node -- have the same
+            // B-row pattern, and would collide on the same accumulator words)
+            const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
+            const int s = __shfl(st, e & 63);  // all lanes active at the shuffles
+            const int n0 = __shfl(ln, e & 63);
+            const double a = __shfl(av, e & 63);
+            const int n = e < nloc ? n0 : 0;
             run_segment(f, s, n, gl, G, a);
         }
     }
@@ -535,12 +567,155 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
         }
         __syncthreads();
         const int nloc = min(64, a1 - jb);
-        for (int e = grp; e < nloc; e += ngrp) {
+        const int iters = (nloc + ngrp - 1) / ngrp;
+        for (int it = 0; it < iters; ++it) {
+            const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
+            if (e >= nloc) continue;
             const int4 v = stage[e];
             run_segment(f, v.x, v.y, gl, G, __hiloint2double(v.w, v.z));
         }
         __syncthreads();
     }
+}
+
+// Flattened walk (long B segments): the products of the chunk's A entries are
+// laid end to end; a batch is 64 consecutive products, one per lane, so one
+// load instruction touches at most a couple of B rows (coalesced, every lane
+// busy).  The A entries overlapping a batch are found with a short uniform
+// loop over the chunk's inclusive prefix of segment lengths (readlane on a
+// wave, broadcast LDS reads on a block); U batches issue their loads together.
+template <class F>
+__device__ __forceinline__ void for_products_flat(const WaveTeam&, int a0, int a1,
+                                                  const int* __restrict__ Acol,
+                                                  const double* __restrict__ Aval,
+                                                  const int4* __restrict__ bmeta, bool tiles,
+                                                  const F& f, int4*) {
+    constexpr int U = 2;
+    const int lane = lane_id();
+    for (int jb = a0; jb < a1; jb += 64) {
+        const int jl = jb + lane;
+        int st = 0, ln = 0;
+        double av = 0.0;
+        if (jl < a1) {
+            const int k = Acol[jl];
+            const int4 m = bmeta[k];
+            st = m.x;
+            ln = tiles ? m.z : m.y;
+            if (Aval) av = Aval[jl];
+        }
+        const int nloc = min(64, a1 - jb);
+        const int incl = wave_incl_scan(ln);
+        const int excl = incl - ln;
+        const int avlo = __double2loint(av), avhi = __double2hiint(av);
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+        int jj = 0;  // first entry whose range ends after the current batch start
+        for (int P0 = 0; P0 < total; P0 += 64 * U) {
+            int idx[U];
+            double aa[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int B0 = P0 + 64 * u;
+                const int p = B0 + lane;
+                idx[u] = -1;
+                aa[u] = 0.0;
+                while (jj < nloc && __builtin_amdgcn_readlane(incl, jj) <= B0) ++jj;
+                for (int j2 = jj; j2 < nloc; ++j2) {
+                    const int s = __builtin_amdgcn_readlane(excl, j2);
+                    if (s >= B0 + 64) break;
+                    const int e = __builtin_amdgcn_readlane(incl, j2);
+                    if (p >= s && p < e) {
+                        idx[u] = __builtin_amdgcn_readlane(st, j2) + (p - s);
+                        aa[u] = __hiloint2double(__builtin_amdgcn_readlane(avhi, j2),
+                                                 __builtin_amdgcn_readlane(avlo, j2));
+                    }
+                }
+            }
+            // loads unconditional (clamped index): a branch around each load would
+            // make hipcc wait vmcnt(0) per element and serialise the batch
+            typename F::Item x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = f.load(idx[u] >= 0 ? idx[u] : 0);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (idx[u] >= 0) f.put(x[u], aa[u]);
+        }
+    }
+}
+
+template <int T, bool GM, class F>
+__device__ __forceinline__ void for_products_flat(const BlockTeam<T, GM>&, int a0, int a1,
+                                                  const int* __restrict__ Acol,
+                                                  const double* __restrict__ Aval,
+                                                  const int4* __restrict__ bmeta, bool tiles,
+                                                  const F& f, int4* stage) {
+    constexpr int U = 2;
+    constexpr int W = T / 64;
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    for (int jb = a0; jb < a1; jb += 64) {
+        if (threadIdx.x < 64) {  // wave 0 stages the chunk: {start, incl prefix, a lo, a hi}
+            const int jl = jb + lane;
+            int st = 0, ln = 0;
+            double av = 0.0;
+            if (jl < a1) {
+                const int k = Acol[jl];
+                const int4 m = bmeta[k];
+                st = m.x;
+                ln = tiles ? m.z : m.y;
+                if (Aval) av = Aval[jl];
+            }
+            const int incl = wave_incl_scan(ln);
+            stage[lane] = make_int4(st, incl, __double2loint(av), __double2hiint(av));
+        }
+        __syncthreads();
+        const int nloc = min(64, a1 - jb);
+        const int total = stage[63].y;
+        int jj = 0;
+        for (int P0 = 64 * U * wv; P0 < total; P0 += 64 * U * W) {
+            int idx[U];
+            double aa[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int B0 = P0 + 64 * u;
+                const int p = B0 + lane;
+                idx[u] = -1;
+                aa[u] = 0.0;
+                while (jj < nloc && stage[jj].y <= B0) ++jj;
+                for (int j2 = jj; j2 < nloc; ++j2) {
+                    const int4 v = stage[j2];
+                    const int s = j2 ? stage[j2 - 1].y : 0;
+                    if (s >= B0 + 64) break;
+                    if (p >= s && p < v.y) {
+                        idx[u] = v.x + (p - s);
+                        aa[u] = __hiloint2double(v.w, v.z);
+                    }
+                }
+            }
+            // loads unconditional (clamped index): a branch around each load would
+            // make hipcc wait vmcnt(0) per element and serialise the batch
+            typename F::Item x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = f.load(idx[u] >= 0 ? idx[u] : 0);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (idx[u] >= 0) f.put(x[u], aa[u]);
+        }
+        __syncthreads();
+    }
+}
+
+// Lane groups (the flattened walk is kept as an experiment: its per-batch
+// owner search costs more instructions than it saves in coalescing).
+template <class Team, class F>
+__device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
+                                              const int* __restrict__ Acol,
+                                              const double* __restrict__ Aval,
+                                              const int4* __restrict__ bmeta, bool tiles,
+                                              long long work, const F& f, int4* stage) {
+    const int nA = a1 - a0;
+    if (MHS_NUM_DIAG == 6 && nA > 0 && work >= 8LL * nA)  // flattened walk: experiment only (slower)
+        for_products_flat(tm, a0, a1, Acol, Aval, bmeta, tiles, f, stage);
+    else
+        for_products(tm, a0, a1, Acol, Aval, bmeta, tiles, pick_group(work, nA, Team::size), f, stage);
 }
 
 // ---------------------------------------------------------- tile tables ---
@@ -576,32 +751,55 @@ struct TileBuild {
     }
 };
 
-// Numeric: product (c, a*b) -> acc[base(tile(c)) + popc(mask & below(c))].
-template <bool GM>
+// Numeric accumulate, one functor per row mode (compile-time: no per-product
+// mode branch).  DENSE: acc[col - colbase].  DIRECT / HASH: product (c, a*b)
+// -> acc[base(tile(c)) + popc(mask & below(c))], the tile found direct-mapped
+// or by probing (always present: it was inserted by the tile build).
+template <bool GM, int MODE>
 struct Accum {
     const TileEntry* E;
     double* acc;
-    bool direct;
-    int lo, H, hshift;
+    int lo, H, hshift, colbase;
     const int* __restrict__ Bcol;
     const double* __restrict__ Bval;
     struct Item {
         int c;
         double v;
     };
-    __device__ __forceinline__ Item load(int i) const { return Item{Bcol[i], Bval[i]}; }
+    __device__ __forceinline__ Item load(int i) const {
+#if MHS_NUM_DIAG == 4  // diagnostic build: no B loads
+        return Item{colbase + (i & 63), (double)i};
+#else
+        return Item{Bcol[i], Bval[i]};
+#endif
+    }
     __device__ __forceinline__ void put(const Item& x, double a) const {
-        const int tc = x.c >> TILE_SHIFT;
-        int s;
-        if (direct) {
-            s = tc - lo;
+#if MHS_NUM_DIAG == 3  // diagnostic build: no LDS work at all
+        asm volatile("" ::"v"(x.c), "v"(a * x.v));
+        return;
+#endif
+        int idx;
+        if constexpr (MODE == NM_DENSE) {
+            idx = x.c - colbase;
         } else {
-            s = hslot(tc, hshift);
-            while (E[s].key != tc) s = (s + 1) & (H - 1);
+            const int tc = x.c >> TILE_SHIFT;
+            int s;
+            if constexpr (MODE == NM_DIRECT) {
+                s = tc - lo;
+            } else {
+                s = hslot(tc, hshift);
+                while (E[s].key != tc) s = (s + 1) & (H - 1);
+            }
+            const uint4 q = *reinterpret_cast<const uint4*>(&E[s]);  // one ds_read_b128
+            const unsigned long long mask = ((unsigned long long)q.y << 32) | q.x;
+            const unsigned long long below = (1ull << (x.c & (TILE_BITS - 1))) - 1;
+            idx = (int)q.z + __popcll(mask & below);
         }
-        const TileEntry e = E[s];
-        const unsigned long long below = (1ull << (x.c & (TILE_BITS - 1))) - 1;
-        acc_add<GM>(&acc[e.base + __popcll(e.mask & below)], a * x.v);
+#if MHS_NUM_DIAG == 1  // diagnostic build: plain LDS store instead of the atomic add
+        acc[idx] = a * x.v;
+#else
+        acc_add<GM>(&acc[idx], a * x.v);
+#endif
     }
 };
 
@@ -614,8 +812,7 @@ __device__ __forceinline__ void build_tiles(const Team& tm, TileEntry* E, bool d
                                             const unsigned long long* __restrict__ btmask,
                                             int tflop, int4* stage) {
     const TileBuild f{E, direct, lo, H, hshift, btcol, btmask};
-    for_products(tm, a0, a1, Acol, nullptr, bmeta, true, pick_group(tflop, a1 - a0, Team::size), f,
-                 stage);
+    walk_products(tm, a0, a1, Acol, nullptr, bmeta, true, tflop, f, stage);
 }
 
 template <class Team>
@@ -651,16 +848,18 @@ struct SymArgs {
 
 template <class Team>
 __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E, int4* stage) {
-    const int lo = a.rlo[row], hi = a.rhi[row];
+    const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
+    const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
     const int span = hi - lo + 1;
-    const int tflop = a.rtflop[row];
+    const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
     const bool direct = sym_direct(span, tflop);
     const int H = direct ? span : hash_slots(tflop < span ? tflop : span);
     const int hshift = direct ? 0 : ilog2(H);
     clear_tiles(tm, E, H);
     tm.sync();
-    build_tiles(tm, E, direct, lo, H, hshift, a.Aptr[row], a.Aptr[row + 1], a.Acol, a.bmeta,
-                a.btcol, a.btmask, tflop, stage);
+    build_tiles(tm, E, direct, lo, H, hshift, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
+                __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]), a.Acol, a.bmeta, a.btcol, a.btmask,
+                tflop, stage);
     tm.sync();
     long long n = 0;
     int t = 0;
@@ -687,7 +886,7 @@ __global__ __launch_bounds__(256) void k_sym_wave(SymArgs a) {
     const int* list = a.list + a.stats->sym_start[a.bin];
     WaveTeam tm;
     for (RowWalk rw(count, WPB, w); rw.first < rw.end; rw.first += rw.stride)
-        sym_row(tm, a, list[rw.first], E, nullptr);
+        sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, nullptr);
 }
 
 template <int T, bool GLOBALMEM>
@@ -700,7 +899,7 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
     const int* list = a.list + a.stats->sym_start[a.bin];
     int4* stage = (int4*)(smem + 1024);
     for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
-        sym_row(tm, a, list[rw.first], E, stage);
+        sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
 }
 
 // ----------------------------------------------------- scan + classify ---
@@ -751,9 +950,10 @@ __global__ __launch_bounds__(1024) void k_scan_top(int nb, long long* __restrict
     }
 }
 
-__device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed) {
+__device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
+                                          int dense_span_max) {
     if (n == 0) return NUM_NONE;
-    const long long need = num_need(span, t, n);
+    const long long need = num_need(span, t, n, dense_span_max);
     if (need <= NUM_W4_BYTES - WAVE_HDR && flop <= NUM_W4_WORK) return NUM_W4;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16;
     if (need <= NUM_B256_BYTES - BLOCK_HDR && flop <= NUM_B256_WORK) return NUM_B256;
@@ -771,7 +971,7 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
                                                      const int* __restrict__ rhi,
                                                      const int* __restrict__ ctiles,
                                                      unsigned char* __restrict__ bin_id,
-                                                     Stats* __restrict__ stats) {
+                                                     Stats* __restrict__ stats, int dense_span_max) {
     constexpr int PER = SCAN_ITEMS / 1024;
     __shared__ long long ws[16];
     const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -798,7 +998,8 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
             const int n = v[k];
             const int lo = rlo[i], hi = rhi[i];
             const int span = n ? hi - lo + 1 : 0;
-            bin_id[i] = (unsigned char)num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need);
+            bin_id[i] = (unsigned char)num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need,
+                                                  dense_span_max);
         }
         off += v[k];
     }
@@ -826,33 +1027,33 @@ struct NumArgs {
     double* Cval;
     char* gscratch;
     long long gbytes;
+    int dense_span_max;
 };
 
-template <class Team, bool GLOBALMEM>
-__device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region, int* counter,
-                        int4* stage) {
-    const int lo = a.rlo[row], hi = a.rhi[row];
-    const int span = hi - lo + 1;
-    const int t = a.ctiles[row];
-    const int c0 = a.Cptr[row];
-    const int n = a.Cptr[row + 1] - c0;
-    const bool direct = num_direct(span, t, n);
-    const int H = direct ? span : hash_slots(t);
-    const int hshift = direct ? 0 : ilog2(H);
+template <class Team, bool GLOBALMEM, int MODE>
+__device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, int span, int t,
+                             int c0, int n, int a0, int a1, char* region, int* counter,
+                             int4* stage) {
+    MHS_STAMP0();
+    const int H = MODE == NM_HASH ? hash_slots(t) : span;
+    const int hshift = MODE == NM_HASH ? ilog2(H) : 0;
+    const int colbase = lo << TILE_SHIFT;
     TileEntry* E = (TileEntry*)region;
     double* acc = (double*)(region + (long long)H * 16);
-    const int a0 = a.Aptr[row], a1 = a.Aptr[row + 1];
+    const int nacc = MODE == NM_DENSE ? span * TILE_BITS : n;
 
     // 1. the C row's tile table (same as the symbolic pass)
+    MHS_STAMP(0);
     clear_tiles(tm, E, H);
-    if (!direct && tm.rank() == 0) *counter = 0;
+    if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
     tm.sync();
-    build_tiles(tm, E, direct, lo, H, hshift, a0, a1, a.Acol, a.bmeta, a.btcol, a.btmask,
+    build_tiles(tm, E, MODE != NM_HASH, lo, H, hshift, a0, a1, a.Acol, a.bmeta, a.btcol, a.btmask,
                 a.rtflop[row], stage);
     tm.sync();
+    MHS_STAMP(1);
 
     // 2. rank of every tile's first column = prefix popcount in tile order
-    if (direct) {
+    if constexpr (MODE != NM_HASH) {
         tm.exclusive_scan(
             span, [&](int i) { return (int)__popcll(E[i].mask); },
             [&](int i, int v) { E[i].base = v; });
@@ -874,44 +1075,83 @@ __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region,
             [&](int e, int v) { E[(int)(unsigned)S[e]].base = v; });
     }
     tm.sync();
-    for (int r = tm.rank(); r < n; r += Team::size) acc[r] = 0.0;
+    MHS_STAMP(2);
+    for (int r = tm.rank(); r < nacc; r += Team::size) acc[r] = 0.0;
     tm.sync();
+    MHS_STAMP(3);
 
-    // 3. accumulate: product (c, a*b) -> acc[base(tile) + popc(mask & below(c))]
+    // 3. accumulate every product of the row
     {
-        const Accum<GLOBALMEM> f{E, acc, direct, lo, H, hshift, a.Bcol, a.Bval};
-        for_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false,
-                     pick_group(a.rflop[row], a1 - a0, Team::size), f, stage);
+        const Accum<GLOBALMEM, MODE> f{E, acc, lo, H, hshift, colbase, a.Bcol, a.Bval};
+        walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
     }
     tm.sync();
+    MHS_STAMP(4);
 
-    // 4. write C: values straight from the accumulator, columns from the tiles
-    for (int r = tm.rank(); r < n; r += Team::size) a.Cval[c0 + r] = acc[r];
-    if (n >= 8 * t) {
-        // dense masks: one wave per tile, lane = bit
+    // 4. write C (sorted by construction: tiles in column order, bits in order)
+    if constexpr (MODE == NM_DENSE) {
+        // one wave per tile, lane = bit: compaction of the dense accumulator
         const int lane = lane_id();
         const int nw = Team::size / 64, wv = tm.rank() >> 6;
-        for (int s = wv; s < H; s += nw) {
+        for (int s = wv; s < span; s += nw) {
             const TileEntry e = E[s];
-            const int key = direct ? lo + s : e.key;
-            if (e.mask && ((e.mask >> lane) & 1ull))
-                a.Ccol[c0 + e.base + __popcll(e.mask & lanemask_lt())] = (key << TILE_SHIFT) + lane;
+            if ((e.mask >> lane) & 1ull) {
+                const int pos = c0 + e.base + __popcll(e.mask & lanemask_lt());
+                a.Ccol[pos] = colbase + (s << TILE_SHIFT) + lane;
+                a.Cval[pos] = acc[(s << TILE_SHIFT) + lane];
+            }
         }
     } else {
-        for (int s = tm.rank(); s < H; s += Team::size) {
-            const TileEntry e = E[s];
-            unsigned long long mk = e.mask;
-            if (!mk) continue;
-            const int key = direct ? lo + s : e.key;
-            int r = c0 + e.base;
-            while (mk) {
-                const int b = __builtin_ctzll(mk);
-                a.Ccol[r++] = (key << TILE_SHIFT) + b;
-                mk &= mk - 1;
+        for (int r = tm.rank(); r < n; r += Team::size) a.Cval[c0 + r] = acc[r];
+        if (n >= 8 * t) {
+            // dense masks: one wave per tile, lane = bit
+            const int lane = lane_id();
+            const int nw = Team::size / 64, wv = tm.rank() >> 6;
+            for (int s = wv; s < H; s += nw) {
+                const TileEntry e = E[s];
+                const int key = MODE == NM_DIRECT ? lo + s : e.key;
+                if (e.mask && ((e.mask >> lane) & 1ull))
+                    a.Ccol[c0 + e.base + __popcll(e.mask & lanemask_lt())] = (key << TILE_SHIFT) + lane;
+            }
+        } else {
+            for (int s = tm.rank(); s < H; s += Team::size) {
+                const TileEntry e = E[s];
+                unsigned long long mk = e.mask;
+                if (!mk) continue;
+                const int key = MODE == NM_DIRECT ? lo + s : e.key;
+                int r = c0 + e.base;
+                while (mk) {
+                    const int b = __builtin_ctzll(mk);
+                    a.Ccol[r++] = (key << TILE_SHIFT) + b;
+                    mk &= mk - 1;
+                }
             }
         }
     }
     tm.sync();
+    MHS_STAMP(5);
+}
+
+// Row-level scalars are made provably wave-uniform (readfirstlane) so that the
+// mode dispatch and every per-row loop bound compile to scalar control flow.
+template <class Team, bool GLOBALMEM>
+__device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region, int* counter,
+                        int4* stage) {
+    const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
+    const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
+    const int span = hi - lo + 1;
+    const int t = __builtin_amdgcn_readfirstlane(a.ctiles[row]);
+    const int c0 = __builtin_amdgcn_readfirstlane(a.Cptr[row]);
+    const int n = __builtin_amdgcn_readfirstlane(a.Cptr[row + 1]) - c0;
+    const int a0 = __builtin_amdgcn_readfirstlane(a.Aptr[row]);
+    const int a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
+    const int mode = num_mode(span, t, n, a.dense_span_max);
+    if (mode == NM_DENSE)
+        num_row_body<Team, GLOBALMEM, NM_DENSE>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
+    else if (mode == NM_DIRECT)
+        num_row_body<Team, GLOBALMEM, NM_DIRECT>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
+    else
+        num_row_body<Team, GLOBALMEM, NM_HASH>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
 }
 
 template <int BYTES>
@@ -921,7 +1161,8 @@ __global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
     char* reg = smem + w * BYTES;
     WaveTeam tm;
     for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride)
-        num_row<WaveTeam, false>(tm, a, a.list[rw.first], reg + WAVE_HDR, (int*)reg, nullptr);
+        num_row<WaveTeam, false>(tm, a, __builtin_amdgcn_readfirstlane(a.list[rw.first]), reg + WAVE_HDR,
+                                 (int*)reg, nullptr);
 }
 
 template <int T, bool GLOBALMEM>
@@ -932,7 +1173,8 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
     int* counter = (int*)(smem + 128);
     int4* stage = (int4*)(smem + 1024);
     for (RowWalk rw(a.count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
-        num_row<BlockTeam<T, GLOBALMEM>, GLOBALMEM>(tm, a, a.list[rw.first], reg, counter, stage);
+        num_row<BlockTeam<T, GLOBALMEM>, GLOBALMEM>(tm, a, __builtin_amdgcn_readfirstlane(a.list[rw.first]),
+                                                     reg, counter, stage);
 }
 
 // -------------------------------------------------------------- launchers ---
@@ -1036,18 +1278,19 @@ void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipSt
     hipLaunchKernelGGL((k_sym_block<1024, true>), dim3(global_grid), dim3(1024), BLOCK_HDR, s, a);
 }
 
-void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s) {
+void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max) {
     const int nb = (M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS;
     long long* part = (long long*)w.scan_part;
     hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(1024), 0, s, M, Cptr, part);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, nb, part, w.stats);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.rflop, w.rlo, w.rhi,
-                       w.ctiles, w.bin_id, w.stats);
+                       w.ctiles, w.bin_id, w.stats, dense_span_max);
 }
 
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
-                    double* Cval, hipStream_t s, int global_grid) {
+                    double* Cval, hipStream_t s, int global_grid, int dense_span_max) {
     NumArgs a;
+    a.dense_span_max = dense_span_max;
     a.Aptr = A.ptr;
     a.Acol = A.col;
     a.Aval = A.val;

@@ -12,7 +12,7 @@ import re
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "libmhspgemm.so"
+LIB_PATH = Path(os.environ["MHS_LIB"]) if os.environ.get("MHS_LIB") else HERE / "libmhspgemm.so"
 HEADER = HERE.parent.parent / "include" / "mhspgemm.h"
 
 MHS_OK = 0
