@@ -36,6 +36,7 @@ struct mhs_ctx {
     size_t gscratch_bytes = 0;
     Stats* h_stats = nullptr;  // pinned
     hipEvent_t ev[8] = {};
+    bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays)
     std::vector<std::pair<void*, size_t>> pool;
@@ -113,7 +114,7 @@ void pool_put(mhs_ctx* ctx, void* p) {
 
 struct Layout {
     size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, bin_id, blkcnt, rowlist,
-        scan_part, blkflop, stats, total;
+        scan_part, blkflop, mcache, stats, total;
 };
 
 Layout plan(int M, int MB, long long nnzB) {
@@ -141,6 +142,7 @@ Layout plan(int M, int MB, long long nnzB) {
     L.rowlist = take((size_t)M * 4);
     L.scan_part = take(nscan * 8);
     L.blkflop = take(((size_t)M / 4 + 16) * 8);
+    L.mcache = take((size_t)M * MCACHE_SPAN * 8);
     L.total = o;
     return L;
 }
@@ -193,6 +195,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     }
     ctx->stream = ctx->own_stream;
     if (const char* e = getenv("MHS_DENSE_SPAN")) ctx->dense_span_max = atoi(e);
+    if (getenv("MHS_NO_MCACHE")) ctx->use_mcache = false;
     init_kernel_attributes();
     *out = ctx;
     return MHS_OK;
@@ -297,6 +300,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     w.rowlist = (int*)(ctx->ws + L.rowlist);
     w.scan_part = (int*)(ctx->ws + L.scan_part);
     w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
+    w.mcache = ctx->use_mcache ? (unsigned long long*)(ctx->ws + L.mcache) : nullptr;
     w.stats = (Stats*)(ctx->ws + L.stats);
     w.gscratch = ctx->gscratch;
     w.gscratch_bytes = ctx->gscratch_bytes;

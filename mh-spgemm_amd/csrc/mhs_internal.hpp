@@ -33,7 +33,7 @@ constexpr int SCAN_ITEMS = 4096;// rows per block in the row_ptr scan
 enum SymBin : int { SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_NB = 5 };
 // Numeric bins (by LDS need and product work).
 enum NumBin : int {
-    NUM_NONE = 0, NUM_W4 = 1, NUM_W16 = 2, NUM_B256 = 3, NUM_B1024 = 4, NUM_GLOBAL = 5, NUM_NB = 6
+    NUM_NONE = 0, NUM_WS = 1, NUM_W16 = 2, NUM_B256 = 3, NUM_B1024 = 4, NUM_GLOBAL = 5, NUM_NB = 6
 };
 
 // Per-team LDS budgets (bytes).  The wave kernels carve one region per wave.
@@ -41,8 +41,8 @@ constexpr int SYM_WAVE_BYTES = 4096;
 constexpr int SYM_WAVE_WORK = 4096;     // tile products a single wave takes on
 constexpr int SYM_B256_BYTES = 32768;
 constexpr int SYM_B256_WORK = 1 << 20;
-constexpr int NUM_W4_BYTES = 4096;
-constexpr int NUM_W4_WORK = 8192;       // products a single wave takes on
+constexpr int NUM_WS_BYTES = 5120;   // 4 waves x 5 KiB = 20 KiB/block: 8 blocks (32 waves) per CU
+constexpr int NUM_WS_WORK = 8192;       // products a single wave takes on
 constexpr int NUM_W16_BYTES = 16384;
 constexpr int NUM_W16_WORK = 32768;
 constexpr int NUM_B256_BYTES = 65536;
@@ -113,7 +113,12 @@ __host__ __device__ inline long long sym_need(int span, int tflop) {
 //             (n doubles): a product lands at base(tile) + popc(mask & below(col));
 //   NM_HASH   scattered rows: hashed tile table + rank-compressed accumulator
 //             (tiles sorted by key to assign bases).
-enum NumMode : int { NM_DENSE = 0, NM_DIRECT = 1, NM_HASH = 2 };
+enum NumMode : int { NM_DENSE = 0, NM_DIRECT = 1, NM_HASH = 2, NM_RMAP = 3 };
+constexpr int MCACHE_SPAN = 32;   // rows spanning <= 32 tiles: symbolic keeps their tile masks
+#ifndef MHS_RMAP_SPAN
+#define MHS_RMAP_SPAN 0  // rank map off: measured 25% slower than DIRECT on cant-like
+#endif
+constexpr int RMAP_SPAN_MAX = MHS_RMAP_SPAN; // NM_RMAP: column -> rank map (uint16 per column of the span)
 __host__ __device__ inline long long num_need_dense(int span) { return (long long)span * (16 + 64 * 8); }
 __host__ __device__ inline long long num_need_direct(int span, int n) {
     return (long long)span * 16 + align16((long long)n * 8);
@@ -123,13 +128,20 @@ __host__ __device__ inline long long num_need_hash(int t, int n) {
     const int p = next_pow2(t);
     return (long long)h * 16 + align16((long long)(n > p ? n : p) * 8);
 }
+__host__ __device__ inline long long num_need_rmap(int span, int n) {
+    return (long long)span * 16 + align16((long long)span * 64 * 2) + align16((long long)n * 8);
+}
+// symbolic stores the OR'd tile masks of rows it tabled direct-mapped over a narrow span
+__host__ __device__ inline bool mcached(int span, int tflop) { return span <= MCACHE_SPAN && sym_direct(span, tflop); }
 __host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_max) {
     if (span <= dense_span_max) return NM_DENSE;
+    if (span <= RMAP_SPAN_MAX) return NM_RMAP;
     return num_need_direct(span, n) <= num_need_hash(t, n) ? NM_DIRECT : NM_HASH;
 }
 __host__ __device__ inline long long num_need(int span, int t, int n, int dense_span_max) {
     const int m = num_mode(span, t, n, dense_span_max);
-    return m == NM_DENSE ? num_need_dense(span) : m == NM_DIRECT ? num_need_direct(span, n) : num_need_hash(t, n);
+    return m == NM_DENSE ? num_need_dense(span) : m == NM_RMAP ? num_need_rmap(span, n)
+                                               : m == NM_DIRECT ? num_need_direct(span, n) : num_need_hash(t, n);
 }
 
 // ------------------------------------------------------------ launchers ---
@@ -157,6 +169,7 @@ struct Work {
     int* rowlist;      // M
     int* scan_part;    // block sums of the row_ptr scan (long long stored as 2 ints)
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
+    unsigned long long* mcache;   // [M][MCACHE_SPAN] tile masks of narrow rows (symbolic -> numeric)
     Stats* stats;
     void* gscratch;    // global-bin scratch
     size_t gscratch_bytes;

@@ -38,17 +38,20 @@
 #ifndef MHS_BLOCKDIST
 #define MHS_BLOCKDIST 1  // A entries -> lane groups: 1 block distribution, 0 cyclic
 #endif
-#if MHS_NUM_DIAG == 9  // diagnostic build: per-phase s_memtime cycles of the numeric rows
-__device__ unsigned long long g_diag[8];
+#if MHS_NUM_DIAG == 9  // diagnostic build: per-row, per-phase s_memtime cycles (plain stores)
+__device__ unsigned long long* g_rowdiag;  // [M][8]
 #define MHS_STAMP0() unsigned long long tp_ = __builtin_amdgcn_s_memtime()
 #define MHS_STAMP(k)                                                    \
     do {                                                                \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
-        if (tm.rank() == 0) atomicAdd(&g_diag[k], t_ - tp_);           \
+        if (tm.rank() == 0) g_rowdiag[(size_t)row * 8 + (k)] = t_ - tp_; \
         tp_ = t_;                                                       \
     } while (0)
-extern "C" int mhs_diag_read(unsigned long long* out) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(g_diag));
+extern "C" int mhs_diag_setup(int M, unsigned long long** dev) {
+    hipError_t e = hipMalloc((void**)dev, (size_t)M * 64);
+    if (e == hipSuccess) e = hipMemset(*dev, 0, (size_t)M * 64);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_rowdiag), dev, sizeof(void*));
+    return (int)e;
 }
 #else
 #define MHS_STAMP0()
@@ -759,6 +762,7 @@ template <bool GM, int MODE>
 struct Accum {
     const TileEntry* E;
     double* acc;
+    const unsigned short* rmap;
     int lo, H, hshift, colbase;
     const int* __restrict__ Bcol;
     const double* __restrict__ Bval;
@@ -781,6 +785,8 @@ struct Accum {
         int idx;
         if constexpr (MODE == NM_DENSE) {
             idx = x.c - colbase;
+        } else if constexpr (MODE == NM_RMAP) {
+            idx = rmap[x.c - colbase];  // one ds_read_u16
         } else {
             const int tc = x.c >> TILE_SHIFT;
             int s;
@@ -844,6 +850,7 @@ struct SymArgs {
     int* ctiles;
     char* gscratch;
     long long gbytes;  // per block
+    unsigned long long* mcache;
 };
 
 template <class Team>
@@ -874,6 +881,10 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
         a.Cptr[row] = (int)n;
         a.ctiles[row] = t;
     }
+    // numeric reuses the OR'd masks of narrow rows (span <= 32 < team size: one store per lane)
+    const int r_ = tm.rank();
+    if (direct && span <= MCACHE_SPAN && r_ < span && a.mcache)
+        a.mcache[(size_t)row * MCACHE_SPAN + r_] = E[r_].mask;
     tm.sync();
 }
 
@@ -954,7 +965,7 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
                                           int dense_span_max) {
     if (n == 0) return NUM_NONE;
     const long long need = num_need(span, t, n, dense_span_max);
-    if (need <= NUM_W4_BYTES - WAVE_HDR && flop <= NUM_W4_WORK) return NUM_W4;
+    if (need <= NUM_WS_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WS;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16;
     if (need <= NUM_B256_BYTES - BLOCK_HDR && flop <= NUM_B256_WORK) return NUM_B256;
     if (need <= B1024_BYTES) return NUM_B1024;
@@ -1028,6 +1039,7 @@ struct NumArgs {
     char* gscratch;
     long long gbytes;
     int dense_span_max;
+    const unsigned long long* mcache;
 };
 
 template <class Team, bool GLOBALMEM, int MODE>
@@ -1039,17 +1051,32 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     const int hshift = MODE == NM_HASH ? ilog2(H) : 0;
     const int colbase = lo << TILE_SHIFT;
     TileEntry* E = (TileEntry*)region;
-    double* acc = (double*)(region + (long long)H * 16);
+    unsigned short* rmap = (unsigned short*)(region + (long long)H * 16);
+    double* acc = (double*)(region + (long long)H * 16 +
+                            (MODE == NM_RMAP ? align16((long long)span * TILE_BITS * 2) : 0));
     const int nacc = MODE == NM_DENSE ? span * TILE_BITS : n;
+    const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
 
-    // 1. the C row's tile table (same as the symbolic pass)
+    // 1. the C row's tile table: the symbolic pass's masks when it kept them,
+    //    else rebuilt (same OR pass as symbolic)
     MHS_STAMP(0);
-    clear_tiles(tm, E, H);
-    if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
-    tm.sync();
-    build_tiles(tm, E, MODE != NM_HASH, lo, H, hshift, a0, a1, a.Acol, a.bmeta, a.btcol, a.btmask,
-                a.rtflop[row], stage);
-    tm.sync();
+    if (MODE != NM_HASH && a.mcache && mcached(span, tflop)) {
+        for (int s = tm.rank(); s < span; s += Team::size) {
+            TileEntry z;
+            z.mask = a.mcache[(size_t)row * MCACHE_SPAN + s];
+            z.base = 0;
+            z.key = -1;
+            E[s] = z;
+        }
+        tm.sync();
+    } else {
+        clear_tiles(tm, E, H);
+        if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
+        tm.sync();
+        build_tiles(tm, E, MODE != NM_HASH, lo, H, hshift, a0, a1, a.Acol, a.bmeta, a.btcol, a.btmask,
+                    tflop, stage);
+        tm.sync();
+    }
     MHS_STAMP(1);
 
     // 2. rank of every tile's first column = prefix popcount in tile order
@@ -1075,6 +1102,17 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             [&](int e, int v) { E[(int)(unsigned)S[e]].base = v; });
     }
     tm.sync();
+    if constexpr (MODE == NM_RMAP) {
+        // column -> C-row rank over the span (one wave per tile, lane = bit)
+        const int lane = lane_id();
+        const int nw = Team::size / 64, wv = tm.rank() >> 6;
+        for (int s = wv; s < span; s += nw) {
+            const TileEntry e = E[s];
+            if ((e.mask >> lane) & 1ull)
+                rmap[(s << TILE_SHIFT) + lane] = (unsigned short)(e.base + __popcll(e.mask & lanemask_lt()));
+        }
+        tm.sync();
+    }
     MHS_STAMP(2);
     for (int r = tm.rank(); r < nacc; r += Team::size) acc[r] = 0.0;
     tm.sync();
@@ -1082,7 +1120,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
 
     // 3. accumulate every product of the row
     {
-        const Accum<GLOBALMEM, MODE> f{E, acc, lo, H, hshift, colbase, a.Bcol, a.Bval};
+        const Accum<GLOBALMEM, MODE> f{E, acc, rmap, lo, H, hshift, colbase, a.Bcol, a.Bval};
         walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
     }
     tm.sync();
@@ -1109,7 +1147,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             const int nw = Team::size / 64, wv = tm.rank() >> 6;
             for (int s = wv; s < H; s += nw) {
                 const TileEntry e = E[s];
-                const int key = MODE == NM_DIRECT ? lo + s : e.key;
+                const int key = MODE != NM_HASH ? lo + s : e.key;
                 if (e.mask && ((e.mask >> lane) & 1ull))
                     a.Ccol[c0 + e.base + __popcll(e.mask & lanemask_lt())] = (key << TILE_SHIFT) + lane;
             }
@@ -1118,7 +1156,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                 const TileEntry e = E[s];
                 unsigned long long mk = e.mask;
                 if (!mk) continue;
-                const int key = MODE == NM_DIRECT ? lo + s : e.key;
+                const int key = MODE != NM_HASH ? lo + s : e.key;
                 int r = c0 + e.base;
                 while (mk) {
                     const int b = __builtin_ctzll(mk);
@@ -1148,6 +1186,8 @@ __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region,
     const int mode = num_mode(span, t, n, a.dense_span_max);
     if (mode == NM_DENSE)
         num_row_body<Team, GLOBALMEM, NM_DENSE>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
+    else if (mode == NM_RMAP)
+        num_row_body<Team, GLOBALMEM, NM_RMAP>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
     else if (mode == NM_DIRECT)
         num_row_body<Team, GLOBALMEM, NM_DIRECT>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
     else
@@ -1265,6 +1305,7 @@ void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipSt
     a.ctiles = w.ctiles;
     a.gscratch = (char*)w.gscratch;
     a.gbytes = (long long)sym_global_bytes_per_block(N);
+    a.mcache = w.mcache;
     // Persistent grids: the bin sizes stay on the device (no host round trip);
     // blocks past a bin's rows exit at once.
     a.bin = SYM_WAVE;
@@ -1291,6 +1332,7 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
                     double* Cval, hipStream_t s, int global_grid, int dense_span_max) {
     NumArgs a;
     a.dense_span_max = dense_span_max;
+    a.mcache = w.mcache;
     a.Aptr = A.ptr;
     a.Acol = A.col;
     a.Aval = A.val;
@@ -1333,11 +1375,11 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
         hipLaunchKernelGGL(k_num_wave<NUM_W16_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, 2048)), dim3(256),
                            WPB * NUM_W16_BYTES, s, a);
     }
-    if (h.num_count[NUM_W4] > 0) {
-        a.list = w.rowlist + h.num_start[NUM_W4];
-        a.count = h.num_count[NUM_W4];
-        hipLaunchKernelGGL(k_num_wave<NUM_W4_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, 4096)), dim3(256),
-                           WPB * NUM_W4_BYTES, s, a);
+    if (h.num_count[NUM_WS] > 0) {
+        a.list = w.rowlist + h.num_start[NUM_WS];
+        a.count = h.num_count[NUM_WS];
+        hipLaunchKernelGGL(k_num_wave<NUM_WS_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, 4096)), dim3(256),
+                           WPB * NUM_WS_BYTES, s, a);
     }
 }
 
