@@ -73,6 +73,7 @@ struct Stats {
     long long sym_start[NBINS];
     long long num_start[NBINS];
 };
+constexpr int SAME_PATTERN = 0x40000000;  // bmeta.z flag: B row repeats row-1's columns
 constexpr int ERR_UNSORTED = 1;
 constexpr int ERR_COL_RANGE = 2;
 constexpr int ERR_ACOL_RANGE = 4;

@@ -32,8 +32,20 @@
 #ifndef MHS_NUM_DIAG
 #define MHS_NUM_DIAG 0  // != 0 only in tools/diag timing builds (wrong results by design)
 #endif
+#ifndef MHS_SAMEPAT
+#define MHS_SAMEPAT 1  // detect runs of same-pattern B rows (FEM dof blocks)
+#endif
+#ifndef MHS_RUN_MAX
+#define MHS_RUN_MAX 3  // longest run a value walk merges into one accumulate (1..4)
+#endif
+#ifndef MHS_RUN_UNROLL
+#define MHS_RUN_UNROLL 2  // B entries per lane issued together in a run walk (registers: occupancy)
+#endif
 #ifndef MHS_UNROLL
 #define MHS_UNROLL 4  // B entries per lane issued together in the product walk
+#endif
+#ifndef MHS_NUM_WAVES_EU
+#define MHS_NUM_WAVES_EU 1  // occupancy floor the wave numeric kernel is compiled for
 #endif
 #ifndef MHS_BLOCKDIST
 #define MHS_BLOCKDIST 1  // A entries -> lane groups: 1 block distribution, 0 cyclic
@@ -132,6 +144,75 @@ __device__ __forceinline__ int pick_group(long long work, int nA, int T) {
         }
     }
     return best;
+}
+
+// bmeta.z = tile count | SAME_PATTERN (row has the column pattern of row-1).
+__device__ __forceinline__ int meta_ntiles(const int4& m) { return m.z & ~SAME_PATTERN; }
+__device__ __forceinline__ bool meta_same(const int4& m) { return (m.z & SAME_PATTERN) != 0; }
+// Runs.  A entry j continues a run when Acol[j] = Acol[j-1] + 1 and B row Acol[j]
+// has the column pattern of B row Acol[j]-1 (bmeta SAME_PATTERN, e.g. the dofs of
+// one FEM node).  The rows of a run are consecutive in B's CSR and equally long, so
+// B row k+i starts at s + i*n.  A tile walk visits only the head of each run (the
+// tile masks are the same; OR is idempotent); a value walk visits heads of runs cut
+// every MHS_RUN_MAX entries and sums a_i * b_i over the run before one accumulate.
+struct StagedChunk {
+    int st, ln, L;  // this lane's entry: B segment start, length, run length (heads)
+    double av;
+    int src;        // compacted visit list: src of visit e is in lane e
+    int nh, lmax;   // visits in the chunk, longest run (wave-uniform)
+};
+
+// Lanes hold the chunk entries [jb, jb+64) ∩ [.., a1) of one A row (lane 0 = jb).
+// Loads are issued together (kprev clamped, not branched on) and every lane
+// reaches the ballots.
+__device__ __forceinline__ StagedChunk stage_chunk(int lane, int jb, int a1,
+                                                   const int* __restrict__ Acol,
+                                                   const double* __restrict__ Aval,
+                                                   const int4* __restrict__ bmeta, bool tiles) {
+    StagedChunk x;
+    x.st = 0;
+    x.ln = 0;
+    x.av = 0.0;
+    const int jl = jb + lane;
+    const bool in = jl < a1;
+    bool cont = false;
+    if (in) {
+        const int k = Acol[jl];
+        const int kp = Acol[jl > 0 ? jl - 1 : 0];
+        const int4 m = bmeta[k];
+        x.st = m.x;
+        x.ln = tiles ? meta_ntiles(m) : m.y;
+        cont = MHS_SAMEPAT && lane > 0 && meta_same(m) && kp == k - 1;
+        if (Aval) x.av = Aval[jl];
+    }
+    const unsigned long long C = __ballot(cont);
+    bool head;
+    if (tiles) {
+        head = in && !cont;
+        x.L = 1;
+    } else if (MHS_RUN_MAX == 1) {
+        head = in;
+        x.L = 1;
+    } else {
+        const unsigned long long incl = (2ull << lane) - 1;  // lanes <= lane (all at 63)
+        const int h = 63 - __clzll(~C & incl);               // start of this lane's run
+        head = in && (lane - h) % MHS_RUN_MAX == 0;
+        const unsigned long long above = lane == 63 ? 0ull : (C >> (lane + 1));
+        x.L = min(MHS_RUN_MAX, 1 + __builtin_ctzll(~above));
+    }
+    const unsigned long long Hm = __ballot(head);
+    x.nh = __popcll(Hm);
+    const int ci = __popcll(Hm & lanemask_lt());
+    const int dst = head ? ci : x.nh + (lane - ci);  // a permutation of the lanes
+    x.src = __builtin_amdgcn_ds_permute(dst << 2, lane);
+    int lm = 1;
+    if (!tiles && MHS_RUN_MAX > 1) {
+        if (__ballot(head && x.L > 1)) lm = 2;
+        if (MHS_RUN_MAX > 2 && __ballot(head && x.L > 2)) lm = 3;
+        if (MHS_RUN_MAX > 3 && __ballot(head && x.L > 3)) lm = 4;
+    }
+    x.lmax = lm;
+    return x;
 }
 
 // XCD-grouped walk over a row list: blocks b and b+8 share an XCD (round-robin
@@ -267,17 +348,24 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
-    const unsigned long long gmask = (G == 64) ? ~0ull : (((1ull << G) - 1) << gbase);
+    unsigned long long gmask = ~0ull;
+    if constexpr (G < 64) gmask = ((1ull << G) - 1) << gbase;
     const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
     const bool valid = row < MB;
     const int s = valid ? ptr[row] : 0;
     const int e = valid ? ptr[row + 1] : 0;
+    // same column pattern as the previous row (FEM dofs of one node): later
+    // phases OR its tiles once per run and fuse its products (SAME_PATTERN)
+    const int ps = (valid && row > 0) ? ptr[row - 1] : 0;
+    const bool same_len = valid && row > 0 && e > s && (s - ps) == (e - s);
+    bool differ = false;
     int ntiles = 0, prev_col = -1, err = 0;
     unsigned long long carry = 0;
     for (int b = s; b < e; b += G) {
         const int j = b + gl;
         const bool in = j < e;
         const int c = in ? col[j] : INT_MAX;
+        if (same_len && in && col[ps + (j - s)] != c) differ = true;
         const int up = __shfl_up(c, 1, G);
         const int pc = (gl == 0) ? prev_col : up;
         const int tile = c >> TILE_SHIFT;
@@ -315,8 +403,9 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
         carry = lt ? 0ull : lm;
         prev_col = lc;
     }
+    const bool same = same_len && (__ballot(differ) & gmask) == 0;
     if (valid && gl == 0) {
-        bmeta[row] = make_int4(s, e - s, ntiles, e > s ? (col[s] >> TILE_SHIFT) : INT_MAX);
+        bmeta[row] = make_int4(s, e - s, ntiles | (same ? SAME_PATTERN : 0), e > s ? (col[s] >> TILE_SHIFT) : INT_MAX);
         bhi[row] = e > s ? (col[e - 1] >> TILE_SHIFT) : -1;
     }
     if (__any(err != 0)) {
@@ -365,7 +454,7 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
             }
             const int4 m = bmeta[k];
             flop += m.y;
-            tflop += m.z;
+            tflop += meta_ntiles(m);
             lo = min(lo, m.w);
             hi = max(hi, bhi[k]);
         }
@@ -514,6 +603,46 @@ __device__ __forceinline__ void run_segment(const F& f, int s, int n, int gl, in
     for (; q < n; q += G) f.put(f.load(s + q), a);
 }
 
+// Value walk over one run of LM (compile-time bound) B rows, L (<= LM) of them
+// live: B entry q of row k+i is s + i*n + q.  Loads of dead rows are clamped to
+// row k (a cache hit) rather than branched around.
+template <int LM, class F>
+__device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl, int G,
+                                                const double (&a)[LM], int L) {
+    constexpr int U = LM == 1 ? MHS_UNROLL : MHS_RUN_UNROLL;
+    int o[LM];
+#pragma unroll
+    for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
+    int q = gl;
+    for (; q + (U - 1) * G < n; q += U * G) {
+        int c[U];
+        double b[U][LM];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            c[u] = f.col(s + q + u * G);
+#pragma unroll
+            for (int i = 0; i < LM; ++i) b[u][i] = f.val(s + o[i] + q + u * G);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            double v = a[0] * b[u][0];
+#pragma unroll
+            for (int i = 1; i < LM; ++i) v += i < L ? a[i] * b[u][i] : 0.0;
+            f.add(c[u], v);
+        }
+    }
+    for (; q < n; q += G) {
+        const int c = f.col(s + q);
+        double v = a[0] * f.val(s + q);
+#pragma unroll
+        for (int i = 1; i < LM; ++i) {
+            const double bi = f.val(s + o[i] + q);
+            v += i < L ? a[i] * bi : 0.0;
+        }
+        f.add(c, v);
+    }
+}
+
 template <class F>
 __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
                                              const int* __restrict__ Acol,
@@ -523,28 +652,37 @@ __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
     const int lane = lane_id();
     const int grp = lane / G, gl = lane & (G - 1), ngrp = 64 / G;
     for (int jb = a0; jb < a1; jb += 64) {
-        const int jl = jb + lane;
-        int st = 0, ln = 0;
-        double av = 0.0;
-        if (jl < a1) {
-            const int k = Acol[jl];
-            const int4 m = bmeta[k];
-            st = m.x;
-            ln = tiles ? m.z : m.y;
-            if (Aval) av = Aval[jl];
-        }
-        const int nloc = min(64, a1 - jb);
-        const int iters = (nloc + ngrp - 1) / ngrp;
+        const StagedChunk x = stage_chunk(lane, jb, a1, Acol, Aval, bmeta, tiles);
+        const int iters = (x.nh + ngrp - 1) / ngrp;
         for (int it = 0; it < iters; ++it) {
             // block distribution: groups run A entries far apart in the row at the same
-            // time (consecutive entries -- e.g. the dofs of one FEM node -- have the same
-            // B-row pattern, and would collide on the same accumulator words)
+            // time (neighbouring entries share B columns and would collide on the same
+            // accumulator words)
             const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
-            const int s = __shfl(st, e & 63);  // all lanes active at the shuffles
-            const int n0 = __shfl(ln, e & 63);
-            const double a = __shfl(av, e & 63);
-            const int n = e < nloc ? n0 : 0;
-            run_segment(f, s, n, gl, G, a);
+            const int h = __shfl(x.src, e & 63);  // all lanes active at the shuffles
+            const int s = __shfl(x.st, h);
+            const int n0 = __shfl(x.ln, h);
+            const int n = e < x.nh ? n0 : 0;
+            if constexpr (F::kValues) {
+                const int L = __shfl(x.L, h);
+                if (x.lmax == 1) {
+                    const double a[1] = {__shfl(x.av, h)};
+                    run_segment_run<1>(f, s, n, gl, G, a, 1);
+                } else if (x.lmax == 2) {
+                    const double a[2] = {__shfl(x.av, h), __shfl(x.av, min(h + 1, 63))};
+                    run_segment_run<2>(f, s, n, gl, G, a, L);
+                } else if (x.lmax == 3) {
+                    const double a[3] = {__shfl(x.av, h), __shfl(x.av, min(h + 1, 63)),
+                                         __shfl(x.av, min(h + 2, 63))};
+                    run_segment_run<3>(f, s, n, gl, G, a, L);
+                } else {
+                    const double a[4] = {__shfl(x.av, h), __shfl(x.av, min(h + 1, 63)),
+                                         __shfl(x.av, min(h + 2, 63)), __shfl(x.av, min(h + 3, 63))};
+                    run_segment_run<4>(f, s, n, gl, G, a, L);
+                }
+            } else {
+                run_segment(f, s, n, gl, G, 0.0);
+            }
         }
     }
 }
@@ -556,26 +694,41 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
                                              const int4* __restrict__ bmeta, bool tiles, int G,
                                              const F& f, int4* stage) {
     const int grp = threadIdx.x / G, gl = threadIdx.x & (G - 1), ngrp = T / G;  // ngrp <= 64
+    // stage[-1] = {visits, longest run}; stage[e] = {B start, length, A index, run length}
     for (int jb = a0; jb < a1; jb += 64) {
         if (threadIdx.x < 64) {
-            const int jl = jb + threadIdx.x;
-            int4 v = make_int4(0, 0, 0, 0);
-            if (jl < a1) {
-                const int k = Acol[jl];
-                const int4 m = bmeta[k];
-                const double av = Aval ? Aval[jl] : 0.0;
-                v = make_int4(m.x, tiles ? m.z : m.y, __double2loint(av), __double2hiint(av));
-            }
-            stage[threadIdx.x] = v;
+            const StagedChunk x = stage_chunk(threadIdx.x, jb, a1, Acol, nullptr, bmeta, tiles);
+            const int h = x.src;
+            const int st = __shfl(x.st, h), ln = __shfl(x.ln, h), L = __shfl(x.L, h);
+            if (threadIdx.x < x.nh) stage[threadIdx.x] = make_int4(st, ln, jb + h, L);
+            if (threadIdx.x == 0) stage[-1] = make_int4(x.nh, x.lmax, 0, 0);
         }
         __syncthreads();
-        const int nloc = min(64, a1 - jb);
+        const int4 hd = stage[-1];
+        const int nloc = hd.x, lmax = hd.y;
         const int iters = (nloc + ngrp - 1) / ngrp;
         for (int it = 0; it < iters; ++it) {
             const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
             if (e >= nloc) continue;
             const int4 v = stage[e];
-            run_segment(f, v.x, v.y, gl, G, __hiloint2double(v.w, v.z));
+            if constexpr (F::kValues) {
+                if (lmax == 1) {
+                    const double a[1] = {Aval[v.z]};
+                    run_segment_run<1>(f, v.x, v.y, gl, G, a, 1);
+                } else if (lmax == 2) {
+                    const double a[2] = {Aval[v.z], Aval[v.z + (v.w > 1)]};
+                    run_segment_run<2>(f, v.x, v.y, gl, G, a, v.w);
+                } else if (lmax == 3) {
+                    const double a[3] = {Aval[v.z], Aval[v.z + (v.w > 1)], Aval[v.z + 2 * (v.w > 2)]};
+                    run_segment_run<3>(f, v.x, v.y, gl, G, a, v.w);
+                } else {
+                    const double a[4] = {Aval[v.z], Aval[v.z + (v.w > 1)], Aval[v.z + 2 * (v.w > 2)],
+                                         Aval[v.z + 3 * (v.w > 3)]};
+                    run_segment_run<4>(f, v.x, v.y, gl, G, a, v.w);
+                }
+            } else {
+                run_segment(f, v.x, v.y, gl, G, 0.0);
+            }
         }
         __syncthreads();
     }
@@ -603,7 +756,7 @@ __device__ __forceinline__ void for_products_flat(const WaveTeam&, int a0, int a
             const int k = Acol[jl];
             const int4 m = bmeta[k];
             st = m.x;
-            ln = tiles ? m.z : m.y;
+            ln = tiles ? meta_ntiles(m) : m.y;
             if (Aval) av = Aval[jl];
         }
         const int nloc = min(64, a1 - jb);
@@ -663,7 +816,7 @@ __device__ __forceinline__ void for_products_flat(const BlockTeam<T, GM>&, int a
                 const int k = Acol[jl];
                 const int4 m = bmeta[k];
                 st = m.x;
-                ln = tiles ? m.z : m.y;
+                ln = tiles ? meta_ntiles(m) : m.y;
                 if (Aval) av = Aval[jl];
             }
             const int incl = wave_incl_scan(ln);
@@ -727,6 +880,7 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
 //   hash:   open addressing, Fibonacci hash, linear probe, CAS on the key.
 // Tables hold >= 2x the distinct tiles, so an insert always finds a slot.
 struct TileBuild {
+    static constexpr bool kValues = false;
     TileEntry* E;
     bool direct;
     int lo, H, hshift;
@@ -760,6 +914,7 @@ struct TileBuild {
 // or by probing (always present: it was inserted by the tile build).
 template <bool GM, int MODE>
 struct Accum {
+    static constexpr bool kValues = true;
     const TileEntry* E;
     double* acc;
     const unsigned short* rmap;
@@ -777,11 +932,28 @@ struct Accum {
         return Item{Bcol[i], Bval[i]};
 #endif
     }
-    __device__ __forceinline__ void put(const Item& x, double a) const {
+    __device__ __forceinline__ int col(int i) const {
+#if MHS_NUM_DIAG == 4
+        return colbase + (i & 63);
+#else
+        return Bcol[i];
+#endif
+    }
+    __device__ __forceinline__ double val(int i) const {
+#if MHS_NUM_DIAG == 4
+        return (double)i;
+#else
+        return Bval[i];
+#endif
+    }
+    __device__ __forceinline__ void put(const Item& x, double a) const { add(x.c, a * x.v); }
+    // acc[column c] += v
+    __device__ __forceinline__ void add(int c, double v) const {
 #if MHS_NUM_DIAG == 3  // diagnostic build: no LDS work at all
-        asm volatile("" ::"v"(x.c), "v"(a * x.v));
+        asm volatile("" ::"v"(c), "v"(v));
         return;
 #endif
+        const Item x{c, v};
         int idx;
         if constexpr (MODE == NM_DENSE) {
             idx = x.c - colbase;
@@ -802,9 +974,9 @@ struct Accum {
             idx = (int)q.z + __popcll(mask & below);
         }
 #if MHS_NUM_DIAG == 1  // diagnostic build: plain LDS store instead of the atomic add
-        acc[idx] = a * x.v;
+        acc[idx] = v;
 #else
-        acc_add<GM>(&acc[idx], a * x.v);
+        acc_add<GM>(&acc[idx], v);
 #endif
     }
 };
@@ -1195,7 +1367,7 @@ __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region,
 }
 
 template <int BYTES>
-__global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
+__global__ __launch_bounds__(256, MHS_NUM_WAVES_EU) void k_num_wave(NumArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int w = threadIdx.x >> 6;
     char* reg = smem + w * BYTES;

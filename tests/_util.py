@@ -94,3 +94,55 @@ def bin_zoo(seed: int = 11):
     Acol = np.array([k for r in arows for k in r], np.int32)
     Av = rng.uniform(0.1, 1.0, len(Acol))
     return (M, K, Aptr.astype(np.int32), Acol, Av), (K, N, Bptr.astype(np.int32), Bc.astype(np.int32), Bv)
+
+
+def run_zoo(seed: int = 5, N: int = 40_000):
+    """B whose rows come in groups sharing one column pattern (runs of 1..7 rows,
+    like the dofs of a FEM node), plus decoys: adjacent rows of equal length but
+    different columns, and empty rows.  A rows walk consecutive B rows (runs, cut
+    at 64-entry chunk edges and at the 3-row merge cap), skip rows (runs broken),
+    repeat a row (k, k: not a run) and are long enough to reach the block and
+    global kernels.  Exercises the same-pattern flag of the mask formation and the
+    run walks of the symbolic and numeric phases."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    while len(rows) < 4000:
+        kind = rng.integers(0, 10)
+        if kind == 0:
+            rows.append(np.zeros(0, np.int64))                       # empty row
+            continue
+        ln = int(rng.integers(1, 120))
+        pat = np.unique(rng.integers(0, N, ln))
+        if kind == 1:                                                # decoy: same length, new cols
+            rows.append(pat)
+            alt = np.unique(rng.integers(0, N, 4 * len(pat)))[:len(pat)]
+            rows.append(np.sort(alt))
+            continue
+        rows.extend([pat] * int(rng.integers(1, 8)))                 # a run of 1..7 equal rows
+    K = len(rows)
+    Bptr = np.zeros(K + 1, np.int64)
+    Bptr[1:] = np.cumsum([len(r) for r in rows])
+    Bc = np.concatenate(rows).astype(np.int32)
+    Bv = rng.uniform(0.1, 1.0, len(Bc))
+    arows = []
+    for i in range(600):
+        kind = i % 6
+        s = int(rng.integers(0, K - 400))
+        if kind == 0:
+            arows.append(list(range(s, s + int(rng.integers(1, 40)))))          # wave bins
+        elif kind == 1:
+            arows.append(list(range(s, s + int(rng.integers(60, 140)))))        # crosses chunk edges
+        elif kind == 2:
+            arows.append(sorted(set(rng.integers(s, s + 60, 30).tolist())))     # runs broken by gaps
+        elif kind == 3:
+            arows.append([s, s, s + 1, s + 1, s + 2])                           # repeats: not runs
+        elif kind == 4:
+            arows.append(list(range(s, s + 390)))                               # block / global kernels
+        else:
+            arows.append([])
+    M = len(arows)
+    Aptr = np.zeros(M + 1, np.int64)
+    Aptr[1:] = np.cumsum([len(r) for r in arows])
+    Acol = np.array([k for r in arows for k in r], np.int32)
+    Av = rng.uniform(0.1, 1.0, len(Acol))
+    return (M, K, Aptr.astype(np.int32), Acol, Av), (K, N, Bptr.astype(np.int32), Bc, Bv)

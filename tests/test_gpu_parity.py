@@ -12,7 +12,7 @@ import pytest
 import mhspgemm
 from mhspgemm import synth
 from oracle import oracle as orc
-from _util import GOLDEN, PRODUCT_CASES, bin_zoo, load_golden, random_csr
+from _util import GOLDEN, PRODUCT_CASES, bin_zoo, load_golden, random_csr, run_zoo
 
 pytestmark = pytest.mark.gpu
 
@@ -89,6 +89,22 @@ def test_bin_zoo_every_bin(tool):
     # every symbolic bin (1..4) and numeric bin (1..5) saw rows
     assert all(t.sym_bins[i] > 0 for i in range(0, 5)), t.sym_bins
     assert all(t.num_bins[i] > 0 for i in range(0, 6)), t.num_bins
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_run_zoo_same_pattern_rows(tool, seed):
+    (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = run_zoo(seed)
+    A = mhspgemm.CSR(M, K, Ap, Ac, Av)
+    B = mhspgemm.CSR(K2, N, Bp, Bc, Bv)
+    t = check(tool, A, B)
+    assert t.num_bins[1] > 0 and t.num_bins[3] > 0, t.num_bins  # wave and block kernels saw rows
+
+
+def test_fem_dof_runs_square(tool):
+    # A*A with dof 1..4 per node: runs of every length up to and past the merge cap
+    for dof in (1, 2, 3, 4):
+        A = synth.fem_grid(5, 4, 9, dof=dof)
+        check(tool, A, A)
 
 
 def test_mixed_sign_cancellation_keeps_structure(tool):
