@@ -41,8 +41,23 @@
 #ifndef MHS_RUN_UNROLL
 #define MHS_RUN_UNROLL 2  // B entries per lane issued together in a run walk (registers: occupancy)
 #endif
+#ifndef MHS_TILE_UNROLL
+#define MHS_TILE_UNROLL 2  // tiles per lane issued together in a tile walk
+#endif
 #ifndef MHS_UNROLL
 #define MHS_UNROLL 4  // B entries per lane issued together in the product walk
+#endif
+#ifndef MHS_NUM_WS_GRID
+#define MHS_NUM_WS_GRID 4096  // block cap of the small-row numeric launch
+#endif
+#ifndef MHS_VAL_GMIN
+#define MHS_VAL_GMIN 4  // narrowest lane group of a value walk
+#endif
+#ifndef MHS_RUN_GMIN
+#define MHS_RUN_GMIN 32  // narrowest lane group of a chunk with merged runs
+#endif
+#ifndef MHS_PIPE
+#define MHS_PIPE 0  // software-pipelined value walk
 #endif
 #ifndef MHS_NUM_WAVES_EU
 #define MHS_NUM_WAVES_EU 1  // occupancy floor the wave numeric kernel is compiled for
@@ -128,9 +143,9 @@ __device__ __forceinline__ int sat_int(long long x) { return x > INT_MAX ? INT_M
 // ceil(nA / groups) * ceil(avg B-row length / G) (ties -> wider, better
 // coalesced groups); at most 64 groups so one staged chunk of 64 A entries
 // feeds every group.
-__device__ __forceinline__ int pick_group(long long work, int nA, int T) {
+__device__ __forceinline__ int pick_group(long long work, int nA, int T, int gfloor = 4) {
     int gmin = T / 64;
-    if (gmin < 4) gmin = 4;
+    if (gmin < gfloor) gmin = gfloor;
     if (nA <= 0) return gmin;
     const long long avg = (work + nA - 1) / nA;
     int best = gmin;
@@ -591,7 +606,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(int M, int nb, int nb
 
 template <class F>
 __device__ __forceinline__ void run_segment(const F& f, int s, int n, int gl, int G, double a) {
-    constexpr int U = MHS_UNROLL;
+    constexpr int U = MHS_TILE_UNROLL;
     int q = gl;
     for (; q + (U - 1) * G < n; q += U * G) {
         typename F::Item x[U];
@@ -603,6 +618,10 @@ __device__ __forceinline__ void run_segment(const F& f, int s, int n, int gl, in
     for (; q < n; q += G) f.put(f.load(s + q), a);
 }
 
+// Keep a load unconditional: without a use hipcc sinks a load whose value is only
+// selected under a lane predicate into a branch, with an s_waitcnt vmcnt(0) there.
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+
 // Value walk over one run of LM (compile-time bound) B rows, L (<= LM) of them
 // live: B entry q of row k+i is s + i*n + q.  Loads of dead rows are clamped to
 // row k (a cache hit) rather than branched around.
@@ -613,6 +632,46 @@ __device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl
     int o[LM];
 #pragma unroll
     for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
+#if MHS_PIPE
+    // software pipeline: batch t+1's loads are in flight while batch t accumulates
+    // (indices past the segment are clamped to its first entry and not accumulated)
+    if (gl >= n) return;
+    int c0[U], c1[U];
+    double b0[U][LM], b1[U][LM];
+    auto ld = [&](int q, int (&c)[U], double (&b)[U][LM]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int qq = q + u * G < n ? q + u * G : gl;
+            c[u] = f.col(s + qq);
+#pragma unroll
+            for (int i = 0; i < LM; ++i) b[u][i] = f.val(s + o[i] + qq);
+#pragma unroll
+            for (int i = 1; i < LM; ++i) pin(b[u][i]);
+        }
+    };
+    ld(gl, c0, b0);
+    for (int q = gl;; q += U * G) {
+        const bool more = q + U * G < n;
+        ld(more ? q + U * G : gl, c1, b1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (q + u * G < n) {
+                double v = a[0] * b0[u][0];
+#pragma unroll
+                for (int i = 1; i < LM; ++i) v += i < L ? a[i] * b0[u][i] : 0.0;
+                f.add(c0[u], v);
+            }
+        }
+        if (!more) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            c0[u] = c1[u];
+#pragma unroll
+            for (int i = 0; i < LM; ++i) b0[u][i] = b1[u][i];
+        }
+    }
+    return;
+#endif
     int q = gl;
     for (; q + (U - 1) * G < n; q += U * G) {
         int c[U];
@@ -624,6 +683,10 @@ __device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl
             for (int i = 0; i < LM; ++i) b[u][i] = f.val(s + o[i] + q + u * G);
         }
 #pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 1; i < LM; ++i) pin(b[u][i]);
+#pragma unroll
         for (int u = 0; u < U; ++u) {
             double v = a[0] * b[u][0];
 #pragma unroll
@@ -633,12 +696,14 @@ __device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl
     }
     for (; q < n; q += G) {
         const int c = f.col(s + q);
-        double v = a[0] * f.val(s + q);
+        double b[LM];
 #pragma unroll
-        for (int i = 1; i < LM; ++i) {
-            const double bi = f.val(s + o[i] + q);
-            v += i < L ? a[i] * bi : 0.0;
-        }
+        for (int i = 0; i < LM; ++i) b[i] = f.val(s + o[i] + q);
+#pragma unroll
+        for (int i = 1; i < LM; ++i) pin(b[i]);
+        double v = a[0] * b[0];
+#pragma unroll
+        for (int i = 1; i < LM; ++i) v += i < L ? a[i] * b[i] : 0.0;
         f.add(c, v);
     }
 }
@@ -647,12 +712,16 @@ template <class F>
 __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
                                              const int* __restrict__ Acol,
                                              const double* __restrict__ Aval,
-                                             const int4* __restrict__ bmeta, bool tiles, int G,
+                                             const int4* __restrict__ bmeta, bool tiles, int Grow,
                                              const F& f, int4*) {
     const int lane = lane_id();
-    const int grp = lane / G, gl = lane & (G - 1), ngrp = 64 / G;
     for (int jb = a0; jb < a1; jb += 64) {
         const StagedChunk x = stage_chunk(lane, jb, a1, Acol, Aval, bmeta, tiles);
+        // a chunk with merged runs loads LM rows per lane and sweep: wider groups
+        // keep each load instruction within fewer cache lines
+        const int G = (F::kValues && x.lmax > 1 && Grow < MHS_RUN_GMIN) ? MHS_RUN_GMIN : Grow;
+        const int gs = 31 - __clz(G);  // G is a power of two
+        const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
         const int iters = (x.nh + ngrp - 1) / ngrp;
         for (int it = 0; it < iters; ++it) {
             // block distribution: groups run A entries far apart in the row at the same
@@ -691,21 +760,23 @@ template <int T, bool GM, class F>
 __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, int a1,
                                              const int* __restrict__ Acol,
                                              const double* __restrict__ Aval,
-                                             const int4* __restrict__ bmeta, bool tiles, int G,
+                                             const int4* __restrict__ bmeta, bool tiles, int Grow,
                                              const F& f, int4* stage) {
-    const int grp = threadIdx.x / G, gl = threadIdx.x & (G - 1), ngrp = T / G;  // ngrp <= 64
-    // stage[-1] = {visits, longest run}; stage[e] = {B start, length, A index, run length}
+    // stage[-1] = {visits, longest run, group width}; stage[e] = {B start, length, A index, run length}
     for (int jb = a0; jb < a1; jb += 64) {
         if (threadIdx.x < 64) {
             const StagedChunk x = stage_chunk(threadIdx.x, jb, a1, Acol, nullptr, bmeta, tiles);
             const int h = x.src;
             const int st = __shfl(x.st, h), ln = __shfl(x.ln, h), L = __shfl(x.L, h);
             if (threadIdx.x < x.nh) stage[threadIdx.x] = make_int4(st, ln, jb + h, L);
-            if (threadIdx.x == 0) stage[-1] = make_int4(x.nh, x.lmax, 0, 0);
+            const int G = (F::kValues && x.lmax > 1 && Grow < MHS_RUN_GMIN) ? MHS_RUN_GMIN : Grow;
+            if (threadIdx.x == 0) stage[-1] = make_int4(x.nh, x.lmax, G, 0);
         }
         __syncthreads();
         const int4 hd = stage[-1];
-        const int nloc = hd.x, lmax = hd.y;
+        const int nloc = hd.x, lmax = hd.y, G = hd.z;
+        const int gs = 31 - __clz(G);  // G is a power of two
+        const int grp = threadIdx.x >> gs, gl = threadIdx.x & (G - 1), ngrp = T >> gs;  // ngrp <= 64
         const int iters = (nloc + ngrp - 1) / ngrp;
         for (int it = 0; it < iters; ++it) {
             const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
@@ -871,7 +942,8 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
     if (MHS_NUM_DIAG == 6 && nA > 0 && work >= 8LL * nA)  // flattened walk: experiment only (slower)
         for_products_flat(tm, a0, a1, Acol, Aval, bmeta, tiles, f, stage);
     else
-        for_products(tm, a0, a1, Acol, Aval, bmeta, tiles, pick_group(work, nA, Team::size), f, stage);
+        for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
+                     pick_group(work, nA, Team::size, tiles ? 4 : MHS_VAL_GMIN), f, stage);
 }
 
 // ---------------------------------------------------------- tile tables ---
@@ -1550,7 +1622,7 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
     if (h.num_count[NUM_WS] > 0) {
         a.list = w.rowlist + h.num_start[NUM_WS];
         a.count = h.num_count[NUM_WS];
-        hipLaunchKernelGGL(k_num_wave<NUM_WS_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, 4096)), dim3(256),
+        hipLaunchKernelGGL(k_num_wave<NUM_WS_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, MHS_NUM_WS_GRID)), dim3(256),
                            WPB * NUM_WS_BYTES, s, a);
     }
 }
