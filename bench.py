@@ -21,7 +21,7 @@ One JSON line on rank 0: value = 2*flop / (max over ranks of the time per step).
             workload), achieved = algorithmic bytes per launch (BASELINE.md §2:
             B_alg = 8(M+1) + 20 nnz(A) + 12 flop + 12 nnz(C)) / its average
             duration from hipEvents recorded on the launch stream during the
-            timed steps; traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per launch
+            timed steps (MHS_OPT_NUMERIC_EVENTS); traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per launch
             from the committed PMC pass (profiles/), else null.
   cpu_baseline: the oracle (CPU restatement, "port") on the same matrix, all
             host cores, median of repeats.
@@ -130,21 +130,33 @@ def main():
     nnzC = 0
     gather_ms = None
     if world == 1:
+        from mhspgemm import _lib as L
         A.H2D(local)
+        # timed steps: calls return once the numeric phase is queued (stream-ordered,
+        # no per-call host sync); hipEvents around each numeric phase on the launch stream
+        tool.set_option(L.MHS_OPT_SYNC, 0)
+        tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, max(1, args.steps))
         for _ in range(args.warmup):
-            C, t = mhspgemm.spgemm(tool, A, A, timing=True)
+            C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
             nnzC = C.nnz
             C.release()
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            C, t = mhspgemm.spgemm(tool, A, A, timing=True)
-            numeric_ms.append(t.Numeric)
-            phases.append(t)
+            C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
             C.release()
         barrier()
         elapsed = time.perf_counter() - t0
         t_max = elapsed
+        numeric_ms = tool.numeric_ms(args.steps)
+        # phase breakdown (reference Timing fields): separate, synchronised calls after
+        # the timed region
+        tool.set_option(L.MHS_OPT_SYNC, 1)
+        tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, 0)
+        for _ in range(5):
+            C, t = mhspgemm.spgemm(tool, A, A, timing=True)
+            phases.append(t)
+            C.release()
         nnzC = t.nnzC
     else:
         from mhspgemm import distributed as D
@@ -223,6 +235,7 @@ def main():
               for k in ("mem_alloc", "Form_mask_matrix_B", "symbolic_binning", "Calculate_C_nnz",
                         "numeric_binning", "Malloc_C_col_val", "Numeric", "total_e2e")}
         ph["t_ref_getTotal"] = round(float(np.mean([p.getTotal() for p in phases])), 4)
+        ph["note"] = "5 synchronised calls with per-phase events, after the timed region"
         out["phases_ms"] = ph
         out["bins"] = {"symbolic": phases[-1].sym_bins[:5], "numeric": phases[-1].num_bins[:6]}
         if not args.no_cpu:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 1
+#define MHS_ABI_VERSION 2
 
 typedef enum mhs_status {
     MHS_OK = 0,
@@ -86,13 +86,26 @@ int mhs_ctx_set_stream(mhs_ctx *ctx, void *hip_stream);
 /* Release cached workspace and pooled output buffers. */
 int mhs_ctx_trim(mhs_ctx *ctx);
 
+/* Context options (mhs_ctx_set_option):
+ *   MHS_OPT_SYNC (default 1): mhs_spgemm returns after C is complete.  0: it
+ *     returns once the numeric phase is queued on the context stream (C's
+ *     nnz and arrays are valid; their contents are stream-ordered, as for any
+ *     kernel output).  A call with a timing struct always synchronises.
+ *   MHS_OPT_NUMERIC_EVENTS (default 0): keep hipEvent pairs around the numeric
+ *     phase of the last `value` calls, read with mhs_ctx_numeric_ms. */
+typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2 } mhs_option;
+int mhs_ctx_set_option(mhs_ctx *ctx, int option, int value);
+/* Numeric-phase durations (ms) of the last min(n, recorded) calls, oldest
+ * first; waits for them.  Returns the count written, or -status on error. */
+int mhs_ctx_numeric_ms(mhs_ctx *ctx, float *out, int n);
+
 /* C = A * B on the device.  A, B: device CSR.  On MHS_OK, C->M = A->M,
  * C->N = B->N, C->nnz is set and C->ptr/col/val are fresh device
  * allocations owned by the caller (free with mhs_csr_free, or hand back to
  * the context's pool with mhs_ctx_recycle).  A and B may alias.  B is not
  * modified (unlike the reference, which allocates B.d_tile* in place).
- * Returns after C is complete (the context stream is synchronised).
- * t may be NULL. */
+ * Returns after C is complete (the context stream is synchronised), unless
+ * MHS_OPT_SYNC is 0.  t may be NULL. */
 int mhs_spgemm(mhs_ctx *ctx, const mhs_csr *A, const mhs_csr *B, mhs_csr *C, mhs_timing *t);
 
 /* Free a device CSR produced by mhs_spgemm (hipFree) and zero the struct. */

@@ -35,7 +35,14 @@ struct mhs_ctx {
     char* gscratch = nullptr;
     size_t gscratch_bytes = 0;
     Stats* h_stats = nullptr;  // pinned
+    Published* pub = nullptr;  // fine-grained pinned: Stats handed over by the last pre-numeric kernel
+    Published* d_pub = nullptr;
+    int seq = 0;
     hipEvent_t ev[8] = {};
+    bool sync = true;  // MHS_OPT_SYNC
+    // MHS_OPT_NUMERIC_EVENTS: ring of (start, end) events around the numeric phase
+    std::vector<hipEvent_t> nev;
+    long long ncalls = 0;
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays)
@@ -54,6 +61,26 @@ int fail_hip(mhs_ctx* ctx, hipError_t e, const char* what) {
     std::string m = std::string(what) + ": " + hipGetErrorString(e);
     (void)hipGetLastError();
     return fail(ctx, e == hipErrorOutOfMemory ? MHS_ERR_OOM : MHS_ERR_HIP, m);
+}
+
+// Spin until the device has published call `seq`'s Stats.  Every 256 polls the
+// stream is queried: a fault ends the wait with the HIP error, an idle stream
+// without the publication is an internal error (never spins forever).
+int wait_published(mhs_ctx* ctx, hipStream_t s, int seq) {
+    for (unsigned polls = 1;; ++polls) {
+        if (__atomic_load_n(&ctx->pub->seq, __ATOMIC_ACQUIRE) == seq) return MHS_OK;
+        if ((polls & 255) == 0) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(&ctx->pub->seq, __ATOMIC_ACQUIRE) == seq) return MHS_OK;
+                return fail(ctx, MHS_ERR_HIP, "device did not publish the symbolic statistics");
+            }
+            if (q != hipErrorNotReady) return fail_hip(ctx, q, "waiting for the symbolic phase");
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
 }
 
 #define MHS_HIP(expr)                                                   \
@@ -187,6 +214,10 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->h_stats, sizeof(Stats), hipHostMallocDefault);
+    if (e == hipSuccess)
+        e = hipHostMalloc((void**)&ctx->pub, sizeof(Published), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ctx->d_pub, ctx->pub, 0);
+    if (e == hipSuccess) memset(ctx->pub, 0, sizeof(Published));
     for (int i = 0; e == hipSuccess && i < 8; ++i) e = hipEventCreate(&ctx->ev[i]);
     if (e != hipSuccess) {
         fprintf(stderr, "mhs_ctx_create: %s\n", hipGetErrorString(e));
@@ -208,6 +239,9 @@ void mhs_ctx_destroy(mhs_ctx* ctx) {
     mhs_ctx_trim(ctx);
     for (auto& kv : ctx->sizes) (void)kv;  // outstanding C buffers belong to the caller
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
+    if (ctx->pub) (void)hipHostFree(ctx->pub);
+    for (auto& ev : ctx->nev)
+        if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -325,15 +359,28 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     launch_symbolic(a, w, M, N, out.ptr, s, sym_grid);
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
+    Stats h;
     if (M > 0) {
+        // the numeric bin offsets kernel publishes Stats to pinned host memory; the
+        // host spins on the sequence number (no stream sync, no interrupt wake-up)
+        const int seq = ++ctx->seq;
         launch_scan_classify(M, w, out.ptr, s, ctx->dense_span_max);
-        launch_binning(M, w, 1, s, 0);
+        launch_binning(M, w, 1, s, 0, ctx->d_pub, seq);
+        MHS_HIP(hipGetLastError());
+        if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
+        rc = wait_published(ctx, s, seq);
+        if (rc) {
+            pool_put(ctx, out.ptr);
+            return rc;
+        }
+        memcpy(&h, (const void*)&ctx->pub->stats, sizeof(Stats));
+    } else {
+        MHS_HIP(hipGetLastError());
+        MHS_HIP(hipMemcpyAsync(ctx->h_stats, w.stats, sizeof(Stats), hipMemcpyDeviceToHost, s));
+        if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
+        MHS_HIP(hipStreamSynchronize(s));
+        h = *ctx->h_stats;
     }
-    MHS_HIP(hipGetLastError());
-    MHS_HIP(hipMemcpyAsync(ctx->h_stats, w.stats, sizeof(Stats), hipMemcpyDeviceToHost, s));
-    if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
-    MHS_HIP(hipStreamSynchronize(s));
-    const Stats h = *ctx->h_stats;
     if (h.err) {
         pool_put(ctx, out.ptr);
         std::string m;
@@ -371,11 +418,16 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
 
     // ---- Numeric -------------------------------------------------------------------------
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
+    const int nring = (int)ctx->nev.size() / 2;
+    const int slot = nring ? (int)(ctx->ncalls % nring) : 0;
+    if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
     if (out.nnz > 0)
         launch_numeric(a, b, w, h, out.ptr, out.col, out.val, s, NUM_GLOBAL_GRID, ctx->dense_span_max);
     MHS_HIP(hipGetLastError());
+    if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
+    ++ctx->ncalls;
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[6], s));
-    MHS_HIP(hipStreamSynchronize(s));
+    if (timed || ctx->sync) MHS_HIP(hipStreamSynchronize(s));
     *C = out;
 
     if (timed) {
@@ -409,6 +461,44 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         *t = tm;
     }
     return MHS_OK;
+}
+
+int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
+    if (!ctx) return MHS_ERR_INVALID;
+    switch (option) {
+    case MHS_OPT_SYNC:
+        ctx->sync = value != 0;
+        return MHS_OK;
+    case MHS_OPT_NUMERIC_EVENTS: {
+        if (value < 0 || value > 4096) return fail(ctx, MHS_ERR_INVALID, "numeric event ring size out of [0, 4096]");
+        MHS_HIP(hipSetDevice(ctx->device));
+        MHS_HIP(hipStreamSynchronize(ctx->stream));
+        for (auto& ev : ctx->nev) (void)hipEventDestroy(ev);
+        ctx->nev.assign(2 * (size_t)value, nullptr);
+        for (auto& ev : ctx->nev) MHS_HIP(hipEventCreate(&ev));
+        ctx->ncalls = 0;
+        return MHS_OK;
+    }
+    default:
+        return fail(ctx, MHS_ERR_INVALID, "unknown option");
+    }
+}
+
+int mhs_ctx_numeric_ms(mhs_ctx* ctx, float* out, int n) {
+    if (!ctx || (!out && n > 0)) return -MHS_ERR_INVALID;
+    const long long ring = (long long)ctx->nev.size() / 2;
+    if (ring == 0) return 0;
+    long long have = ctx->ncalls < ring ? ctx->ncalls : ring;
+    if (n < have) have = n;
+    for (long long i = 0; i < have; ++i) {
+        const long long call = ctx->ncalls - have + i;
+        const int slot = (int)(call % ring);
+        if (hipEventSynchronize(ctx->nev[2 * slot + 1]) != hipSuccess) return -MHS_ERR_HIP;
+        float f = 0;
+        if (hipEventElapsedTime(&f, ctx->nev[2 * slot], ctx->nev[2 * slot + 1]) != hipSuccess) return -MHS_ERR_HIP;
+        out[i] = f;
+    }
+    return (int)have;
 }
 
 int mhs_memcpy(mhs_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {

@@ -73,6 +73,13 @@ struct Stats {
     long long sym_start[NBINS];
     long long num_start[NBINS];
 };
+// Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
+// kernel writes it and then `seq`, the host spins on `seq` instead of a stream sync.
+struct Published {
+    Stats stats;
+    int seq;
+    int pad[3];
+};
 constexpr int SAME_PATTERN = 0x40000000;  // bmeta.z flag: B row repeats row-1's columns
 constexpr int ERR_UNSORTED = 1;
 constexpr int ERR_COL_RANGE = 2;
@@ -178,7 +185,8 @@ struct Work {
 
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);
 int launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr);  // returns #blocks
-void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks);  // phase 0 sym, 1 num
+void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks,
+                    Published* pub = nullptr, int seq = 0);  // phase 0 sym, 1 num (publishes Stats)
 void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s,
                      int global_grid);
 void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max);

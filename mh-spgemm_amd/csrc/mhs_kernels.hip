@@ -529,7 +529,8 @@ __global__ __launch_bounds__(1024) void k_bin_offsets(int nb, int nblk, int* __r
                                                       int* __restrict__ out_count,
                                                       long long* __restrict__ out_start,
                                                       const unsigned long long* __restrict__ blkflop,
-                                                      int nflop, unsigned long long* __restrict__ out_flop) {
+                                                      int nflop, unsigned long long* __restrict__ out_flop,
+                                                      const Stats* __restrict__ stats, Published* pub, int seq) {
     __shared__ int ws[16];
     __shared__ int bintot[NBINS];
     __shared__ unsigned long long fs[16];
@@ -571,6 +572,21 @@ __global__ __launch_bounds__(1024) void k_bin_offsets(int nb, int nblk, int* __r
         const int x = threadIdx.x;
         out_count[x] = x < nb ? bintot[x] : 0;
         out_start[x] = x < nb ? (long long)blkcnt[x * nblk] : 0;
+    }
+    if (pub) {  // Stats are final: hand them to the host (L1-bypassing reads, system-scope release)
+        __threadfence();
+        __syncthreads();
+        constexpr int NW = (int)(sizeof(Stats) / 4);
+        static_assert(sizeof(Stats) % 4 == 0 && NW <= 1024, "Stats is copied one word per thread");
+        const int* src = reinterpret_cast<const int*>(stats);
+        int* dst = reinterpret_cast<int*>(&pub->stats);
+        if (threadIdx.x < NW)
+            __hip_atomic_store(dst + threadIdx.x,
+                               __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1505,7 +1521,7 @@ int launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr
     return (int)grid.x;
 }
 
-void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks) {
+void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks, Published* pub, int seq) {
     if (M <= 0) return;
     const int nb = phase == 0 ? SYM_NB : NUM_NB;
     const int nblk = (M + BIN_BLOCK - 1) / BIN_BLOCK;
@@ -1513,7 +1529,7 @@ void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_bl
     int* cnt = phase == 0 ? w.stats->sym_count : w.stats->num_count;
     long long* st = phase == 0 ? w.stats->sym_start : w.stats->num_start;
     hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, nb, nblk, w.blkcnt, cnt, st, w.blkflop,
-                       phase == 0 ? nflop_blocks : 0, &w.stats->flop);
+                       phase == 0 ? nflop_blocks : 0, &w.stats->flop, w.stats, pub, seq);
     hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(BIN_BLOCK), 0, s, M, nb, nblk, w.bin_id, w.blkcnt, w.rowlist);
 }
 

@@ -22,6 +22,9 @@ MHS_ERR_INVALID = 3
 MHS_ERR_OVERFLOW = 4
 MHS_ERR_IO = 5
 
+MHS_OPT_SYNC = 1
+MHS_OPT_NUMERIC_EVENTS = 2
+
 STATUS_NAMES = {0: "MHS_OK", 1: "MHS_ERR_HIP", 2: "MHS_ERR_OOM", 3: "MHS_ERR_INVALID",
                 4: "MHS_ERR_OVERFLOW", 5: "MHS_ERR_IO"}
 
@@ -103,6 +106,10 @@ def lib() -> ctypes.CDLL:
     L.mhs_memcpy.restype = c_int
     L.mhs_device_alloc.argtypes = [c_void_p, P(c_void_p), c_size_t]
     L.mhs_device_alloc.restype = c_int
+    L.mhs_ctx_set_option.argtypes = [c_void_p, c_int, c_int]
+    L.mhs_ctx_set_option.restype = c_int
+    L.mhs_ctx_numeric_ms.argtypes = [c_void_p, P(ctypes.c_float), c_int]
+    L.mhs_ctx_numeric_ms.restype = c_int
     L.mhs_device_free.argtypes = [c_void_p, c_void_p]
     L.mhs_device_free.restype = c_int
     _lib = L

@@ -57,6 +57,19 @@ class Tool:
     def set_stream(self, hip_stream: int | None):
         _check(self.ctx, L.lib().mhs_ctx_set_stream(self.ctx, hip_stream or None), "mhs_ctx_set_stream")
 
+    def set_option(self, option: int, value: int):
+        """mhs_ctx_set_option: MHS_OPT_SYNC (0: return once the numeric phase is
+        queued) or MHS_OPT_NUMERIC_EVENTS (ring size of numeric-phase events)."""
+        _check(self.ctx, L.lib().mhs_ctx_set_option(self.ctx, option, value), "mhs_ctx_set_option")
+
+    def numeric_ms(self, n: int) -> list[float]:
+        """Numeric-phase durations (ms) of the last n calls (hipEvents on the stream)."""
+        buf = (ctypes.c_float * max(1, n))()
+        k = L.lib().mhs_ctx_numeric_ms(self.ctx, buf, n)
+        if k < 0:
+            _check(self.ctx, -k, "mhs_ctx_numeric_ms")
+        return [float(buf[i]) for i in range(k)]
+
     def allocate(self, B=None, C=None):  # src/Tool.cu:4 -- workspace grows on demand
         return None
 

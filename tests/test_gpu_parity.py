@@ -107,6 +107,29 @@ def test_fem_dof_runs_square(tool):
         check(tool, A, A)
 
 
+def test_unsynced_calls_and_numeric_event_ring(tool):
+    from mhspgemm import _lib as L
+    A = synth.fem_grid(6, 5, 12)
+    A.H2D(tool.device)
+    Cp, Ci, Cv = orc.spgemm(A.ptr, A.col, A.val, A.ptr, A.col, A.val, A.N)
+    tool.set_option(L.MHS_OPT_SYNC, 0)
+    tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, 4)
+    try:
+        outs = [mhspgemm.spgemm(tool, A, A, timing=False)[0] for _ in range(6)]
+        for C in outs:  # each result intact although the calls never waited
+            p, c, v = C.to_host()
+            assert np.array_equal(p, Cp) and np.array_equal(c, Ci)
+            assert mhspgemm.compare_tol(Cp, Ci, Cv, p, c, v, RTOL, ATOL)[0]
+            C.release()
+        ms = tool.numeric_ms(10)
+        assert len(ms) == 4 and all(m > 0 for m in ms), ms
+    finally:
+        tool.set_option(L.MHS_OPT_SYNC, 1)
+        tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, 0)
+    with pytest.raises(mhspgemm.MHSpGEMMError):
+        tool.set_option(99, 1)
+
+
 def test_mixed_sign_cancellation_keeps_structure(tool):
     p, c, v = random_csr(1500, 1500, 10, seed=9, signed=True)
     A = mhspgemm.CSR(1500, 1500, p, c, v)
