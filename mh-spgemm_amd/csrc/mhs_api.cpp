@@ -140,11 +140,11 @@ void pool_put(mhs_ctx* ctx, void* p) {
 }
 
 struct Layout {
-    size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, bin_id, blkcnt, rowlist,
-        scan_part, blkflop, mcache, stats, total;
+    size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, bin_list, scan_part, mcache,
+        stats, blkflop, total;
 };
 
-Layout plan(int M, int MB, long long nnzB) {
+Layout plan(int M, int MB, long long nnzA, long long nnzB) {
     Layout L{};
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -152,7 +152,6 @@ Layout plan(int M, int MB, long long nnzB) {
         o += al(bytes ? bytes : 16);
         return r;
     };
-    const size_t nblk = (size_t)(M + BIN_BLOCK - 1) / BIN_BLOCK + 1;
     const size_t nscan = (size_t)(M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1;
     L.stats = take(sizeof(Stats));
     L.btcol = take((size_t)nnzB * 4);
@@ -164,11 +163,11 @@ Layout plan(int M, int MB, long long nnzB) {
     L.rlo = take((size_t)M * 4);
     L.rhi = take((size_t)M * 4);
     L.ctiles = take((size_t)M * 4);
-    L.bin_id = take((size_t)M);
-    L.blkcnt = take(NBINS * nblk * 4);
-    L.rowlist = take((size_t)M * 4);
+    L.sym_bin = take((size_t)M);
+    static_assert((int)NUM_NB >= (int)SYM_NB, "bin_list holds either phase's bins");
+    L.bin_list = take((size_t)(NUM_NB - 1) * M * 4);
+    L.blkflop = take(((size_t)analyze_blocks(nnzA, M) + 1) * 8);
     L.scan_part = take(nscan * 8);
-    L.blkflop = take(((size_t)M / 4 + 16) * 8);
     L.mcache = take((size_t)M * MCACHE_SPAN * 8);
     L.total = o;
     return L;
@@ -219,6 +218,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ctx->d_pub, ctx->pub, 0);
     if (e == hipSuccess) memset(ctx->pub, 0, sizeof(Published));
     for (int i = 0; e == hipSuccess && i < 8; ++i) e = hipEventCreate(&ctx->ev[i]);
+    if (e == hipSuccess) e = init_kernel_attributes();
     if (e != hipSuccess) {
         fprintf(stderr, "mhs_ctx_create: %s\n", hipGetErrorString(e));
         delete ctx;
@@ -227,7 +227,6 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     ctx->stream = ctx->own_stream;
     if (const char* e = getenv("MHS_DENSE_SPAN")) ctx->dense_span_max = atoi(e);
     if (getenv("MHS_NO_MCACHE")) ctx->use_mcache = false;
-    init_kernel_attributes();
     *out = ctx;
     return MHS_OK;
 }
@@ -311,7 +310,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     out.N = N;
 
     // ---- mem_alloc: workspace (cached across calls) + C.ptr --------------------
-    const Layout L = plan(M, MB, B->nnz);
+    const Layout L = plan(M, MB, A->nnz, B->nnz);
     size_t sym_g_bytes = 0;
     const int sym_grid = sym_global_grid(N, &sym_g_bytes);
     int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
@@ -329,11 +328,11 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     w.rlo = (int*)(ctx->ws + L.rlo);
     w.rhi = (int*)(ctx->ws + L.rhi);
     w.ctiles = (int*)(ctx->ws + L.ctiles);
-    w.bin_id = (unsigned char*)(ctx->ws + L.bin_id);
-    w.blkcnt = (int*)(ctx->ws + L.blkcnt);
-    w.rowlist = (int*)(ctx->ws + L.rowlist);
-    w.scan_part = (int*)(ctx->ws + L.scan_part);
+    w.sym_bin = (unsigned char*)(ctx->ws + L.sym_bin);
+    w.bin_list = (int*)(ctx->ws + L.bin_list);
     w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
+    w.nflop = M > 0 ? analyze_blocks(A->nnz, M) : 0;
+    w.scan_part = (int*)(ctx->ws + L.scan_part);
     w.mcache = ctx->use_mcache ? (unsigned long long*)(ctx->ws + L.mcache) : nullptr;
     w.stats = (Stats*)(ctx->ws + L.stats);
     w.gscratch = ctx->gscratch;
@@ -352,8 +351,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     launch_mask_b(b, w, s);
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[1], s));
     // ---- symbolic_binning ---------------------------------------------------------
-    const int nflop_blocks = launch_analyze(a, w, MB, s, out.ptr);
-    launch_binning(M, w, 0, s, nflop_blocks);
+    launch_analyze(a, w, MB, s, out.ptr);
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[2], s));
     // ---- Calculate_C_nnz ------------------------------------------------------------
     launch_symbolic(a, w, M, N, out.ptr, s, sym_grid);
@@ -364,8 +362,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         // the numeric bin offsets kernel publishes Stats to pinned host memory; the
         // host spins on the sequence number (no stream sync, no interrupt wake-up)
         const int seq = ++ctx->seq;
-        launch_scan_classify(M, w, out.ptr, s, ctx->dense_span_max);
-        launch_binning(M, w, 1, s, 0, ctx->d_pub, seq);
+        launch_scan_classify(M, w, out.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
         MHS_HIP(hipGetLastError());
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
         rc = wait_published(ctx, s, seq);

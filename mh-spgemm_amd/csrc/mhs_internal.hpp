@@ -26,7 +26,6 @@ constexpr int TILE_SHIFT = 6;  // 64-column tiles, one uint64 mask each (wave64 
 constexpr int TILE_BITS = 64;
 constexpr int NBINS = 8;
 constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
-constexpr int BIN_BLOCK = 1024; // rows per block in the binning kernels
 constexpr int SCAN_ITEMS = 4096;// rows per block in the row_ptr scan
 
 // Symbolic bins (by LDS need and tile work).
@@ -65,11 +64,11 @@ struct Stats {
     unsigned long long flop;       // total products
     long long nnzC;                // total C nnz (scan result)
     int err;                       // error bits (ERR_*)
-    int pad0;
+    int scan_done;                 // k_scan_reduce blocks finished (last one scans the partials)
     int sym_count[NBINS];
     int num_count[NBINS];
     int num_global_need;           // max LDS-equivalent bytes of a global numeric row
-    int pad1;
+    int final_done;                // k_scan_final blocks finished (last one publishes)
     long long sym_start[NBINS];
     long long num_start[NBINS];
 };
@@ -172,11 +171,11 @@ struct Work {
     int* rlo;
     int* rhi;
     int* ctiles;
-    unsigned char* bin_id;
-    int* blkcnt;       // NBINS * nblk
-    int* rowlist;      // M
-    int* scan_part;    // block sums of the row_ptr scan (long long stored as 2 ints)
+    unsigned char* sym_bin;  // M: symbolic bin of every row (k_analyze)
+    int* bin_list;           // (NUM_NB-1) * M: bin x's rows at (x-1)*M (symbolic bins, then numeric bins)
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
+    int nflop;                    // their count
+    int* scan_part;    // block sums of the row_ptr scan (long long stored as 2 ints)
     unsigned long long* mcache;   // [M][MCACHE_SPAN] tile masks of narrow rows (symbolic -> numeric)
     Stats* stats;
     void* gscratch;    // global-bin scratch
@@ -184,15 +183,16 @@ struct Work {
 };
 
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);
-int launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr);  // returns #blocks
-void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks,
-                    Published* pub = nullptr, int seq = 0);  // phase 0 sym, 1 num (publishes Stats)
+void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr);
+int analyze_blocks(long long nnzA, int M);
+
 void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s,
                      int global_grid);
-void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max);
+void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max,
+                          Published* pub, int seq);
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
                     int* Ccol, double* Cval, hipStream_t s, int global_grid, int dense_span_max);
 size_t sym_global_bytes_per_block(int N);
-void init_kernel_attributes();
+hipError_t init_kernel_attributes();
 
 }  // namespace mhs

@@ -442,6 +442,20 @@ __device__ __forceinline__ int sym_bin_of(int flop, int tflop, int span) {
     return SYM_GLOBAL;
 }
 
+// Last block of a grid to reach this point (after its writes): returns true in
+// every thread of that block, with the other blocks' writes visible to it.
+__device__ bool last_block_done(int* done) {
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(done, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last) __threadfence();
+    return last;
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __restrict__ Aptr,
                                                  const int* __restrict__ Acol,
@@ -449,8 +463,7 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
                                                  const int* __restrict__ bhi, int* __restrict__ rflop,
                                                  int* __restrict__ rtflop, int* __restrict__ rlo,
                                                  int* __restrict__ rhi, int* __restrict__ ctiles,
-                                                 unsigned char* __restrict__ bin_id,
-                                                 int* __restrict__ Cptr,
+                                                 unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
                                                  unsigned long long* __restrict__ blkflop,
                                                  Stats* __restrict__ stats) {
     const int lane = lane_id();
@@ -489,13 +502,13 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
         rlo[row] = lo;
         rhi[row] = hi;
         const int bin = sym_bin_of(f, tf, span);
-        bin_id[row] = (unsigned char)bin;
+        sym_bin[row] = (unsigned char)bin;
         if (bin == SYM_NONE) {
             Cptr[row] = 0;
             ctiles[row] = 0;
         }
     }
-    // per-block flop partial (one plain store per block; reduced in k_bin_offsets)
+    // per-block flop partial (plain store; summed by the scan's last block)
     __shared__ unsigned long long wsum[4];
     unsigned long long mine = (valid && gl == 0) ? (unsigned long long)flop : 0ull;
     mine = wave_sum(mine);
@@ -507,110 +520,6 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
 
 // ----------------------------------------------------------------- binning ---
 // Stable partition of rows [0, M) by bin id into one list, bin-major.
-
-__global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(int M, int nb, int nblk,
-                                                         const unsigned char* __restrict__ bin_id,
-                                                         int* __restrict__ blkcnt) {
-    __shared__ int cnt[NBINS];
-    if (threadIdx.x < NBINS) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const int i = blockIdx.x * BIN_BLOCK + threadIdx.x;
-    const int id = i < M ? bin_id[i] : 0;
-    for (int x = 1; x < nb; ++x) {
-        const int c = __popcll(__ballot(id == x));
-        if (lane_id() == 0 && c) atomicAdd(&cnt[x], c);
-    }
-    __syncthreads();
-    if (threadIdx.x < nb) blkcnt[threadIdx.x * nblk + blockIdx.x] = threadIdx.x == 0 ? 0 : cnt[threadIdx.x];
-}
-
-// One block: exclusive scan over blkcnt (bin-major), per-bin count / start.
-__global__ __launch_bounds__(1024) void k_bin_offsets(int nb, int nblk, int* __restrict__ blkcnt,
-                                                      int* __restrict__ out_count,
-                                                      long long* __restrict__ out_start,
-                                                      const unsigned long long* __restrict__ blkflop,
-                                                      int nflop, unsigned long long* __restrict__ out_flop,
-                                                      const Stats* __restrict__ stats, Published* pub, int seq) {
-    __shared__ int ws[16];
-    __shared__ int bintot[NBINS];
-    __shared__ unsigned long long fs[16];
-    if (nflop > 0) {  // total products = sum of k_analyze's per-block partials
-        unsigned long long f = 0;
-        for (int i = threadIdx.x; i < nflop; i += 1024) f += blkflop[i];
-        f = wave_sum(f);
-        if (lane_id() == 0) fs[threadIdx.x >> 6] = f;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long t = 0;
-            for (int k = 0; k < 16; ++k) t += fs[k];
-            *out_flop = t;
-        }
-    }
-    const int L = nb * nblk;
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    if (threadIdx.x < NBINS) bintot[threadIdx.x] = 0;
-    __syncthreads();
-    int carry = 0;
-    for (int b = 0; b < L; b += 1024) {
-        const int i = b + threadIdx.x;
-        const int x = i < L ? blkcnt[i] : 0;
-        if (i < L && x) atomicAdd(&bintot[i / nblk], x);
-        const int inc = wave_incl_scan(x);
-        if (lane == 63) ws[w] = inc;
-        __syncthreads();
-        int woff = 0, tot = 0;
-        for (int k = 0; k < 16; ++k) {
-            const int v = ws[k];
-            woff += (k < w) ? v : 0;
-            tot += v;
-        }
-        if (i < L) blkcnt[i] = carry + woff + inc - x;
-        carry += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x < NBINS) {
-        const int x = threadIdx.x;
-        out_count[x] = x < nb ? bintot[x] : 0;
-        out_start[x] = x < nb ? (long long)blkcnt[x * nblk] : 0;
-    }
-    if (pub) {  // Stats are final: hand them to the host (L1-bypassing reads, system-scope release)
-        __threadfence();
-        __syncthreads();
-        constexpr int NW = (int)(sizeof(Stats) / 4);
-        static_assert(sizeof(Stats) % 4 == 0 && NW <= 1024, "Stats is copied one word per thread");
-        const int* src = reinterpret_cast<const int*>(stats);
-        int* dst = reinterpret_cast<int*>(&pub->stats);
-        if (threadIdx.x < NW)
-            __hip_atomic_store(dst + threadIdx.x,
-                               __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-__global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(int M, int nb, int nblk,
-                                                           const unsigned char* __restrict__ bin_id,
-                                                           const int* __restrict__ blkoff,
-                                                           int* __restrict__ list) {
-    __shared__ int wcnt[NBINS][BIN_BLOCK / 64];
-    const int w = threadIdx.x >> 6;
-    const int i = blockIdx.x * BIN_BLOCK + threadIdx.x;
-    const int id = i < M ? bin_id[i] : 0;
-    int myrank = 0;
-    for (int x = 1; x < nb; ++x) {
-        const unsigned long long bal = __ballot(id == x);
-        if (id == x) myrank = __popcll(bal & lanemask_lt());
-        if (lane_id() == 0) wcnt[x][w] = __popcll(bal);
-    }
-    __syncthreads();
-    if (id > 0 && i < M) {
-        int off = blkoff[id * nblk + blockIdx.x];
-        for (int k = 0; k < w; ++k) off += wcnt[id][k];
-        list[off + myrank] = i;
-    }
-}
 
 // ------------------------------------------------------- product walking ---
 // for_products(team, A row [a0, a1), ...) calls f.put(f.load(idx), a_ij) for
@@ -1103,7 +1012,7 @@ struct SymArgs {
     const int* rtflop;
     const int* rlo;
     const int* rhi;
-    const int* list;
+    const int* list;  // bin x's rows at list + (x-1)*M, count in stats->sym_count[x]
     const Stats* stats;
     int bin;
     int* Cptr;
@@ -1154,7 +1063,7 @@ __global__ __launch_bounds__(256) void k_sym_wave(SymArgs a) {
     const int w = threadIdx.x >> 6;
     TileEntry* E = (TileEntry*)(smem + w * BYTES + WAVE_HDR);
     const int count = a.stats->sym_count[a.bin];
-    const int* list = a.list + a.stats->sym_start[a.bin];
+    const int* list = a.list + (long long)(a.bin - 1) * a.M;
     WaveTeam tm;
     for (RowWalk rw(count, WPB, w); rw.first < rw.end; rw.first += rw.stride)
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, nullptr);
@@ -1167,7 +1076,7 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
     TileEntry* E = GLOBALMEM ? (TileEntry*)(a.gscratch + (long long)blockIdx.x * a.gbytes)
                              : (TileEntry*)(smem + BLOCK_HDR);
     const int count = a.stats->sym_count[a.bin];
-    const int* list = a.list + a.stats->sym_start[a.bin];
+    const int* list = a.list + (long long)(a.bin - 1) * a.M;
     int4* stage = (int4*)(smem + 1024);
     for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
@@ -1175,33 +1084,81 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
 
 // ----------------------------------------------------- scan + classify ---
 
-__global__ __launch_bounds__(1024) void k_scan_reduce(int M, const int* __restrict__ Cptr,
-                                                      long long* __restrict__ part) {
-    __shared__ long long ws[16];
-    const int base = blockIdx.x * SCAN_ITEMS;
-    long long s = 0;
-    for (int k = threadIdx.x; k < SCAN_ITEMS; k += 1024) {
-        const int i = base + k;
-        if (i < M) s += Cptr[i];
+// Append a 1024-thread block's SCAN_ITEMS rows (blockIdx*SCAN_ITEMS + j, bins in
+// binof[j]) to contiguous per-bin lists: bin x's rows at list + (x-1)*M, cursor
+// cnt[x].  The block's rows keep row order; one atomic per (block, bin) reserves
+// their places (the grids that call this have M/4096 blocks: little contention).
+template <int NB>
+__device__ void append_block_rows(const unsigned char* binof, long long M, int* __restrict__ cnt,
+                                  int* __restrict__ list) {
+    constexpr int PER = SCAN_ITEMS / 1024;
+    static_assert(PER * 16 == 64 && NB <= 16, "one wave scans one bin's (pass, wave) counts");
+    __shared__ int wc[NB][PER * 16];  // [bin][pass*16 + wave]: members, then exclusive prefix
+    __shared__ int nbase[NB];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    int mybin[PER], rank[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {  // pass k = rows k*1024 + threadIdx.x of the block (row order)
+        mybin[k] = binof[k * 1024 + threadIdx.x];
+        rank[k] = 0;
+        for (int x = 1; x < NB; ++x) {
+            const unsigned long long bal = __ballot(mybin[k] == x);
+            if (mybin[k] == x) rank[k] = __popcll(bal & lanemask_lt());
+            if (lane == 0) wc[x][k * 16 + w] = __popcll(bal);
+        }
     }
-    s = wave_sum(s);
-    if (lane_id() == 0) ws[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        long long t = 0;
-        for (int k = 0; k < 16; ++k) t += ws[k];
-        part[blockIdx.x] = t;
+    if (w >= 1 && w < NB) {  // wave x: exclusive prefix over (pass, wave); reserve the block's places
+        const int c = wc[w][lane];
+        const int inc = wave_incl_scan(c);
+        wc[w][lane] = inc - c;
+        if (lane == 63) nbase[w] = inc ? atomicAdd(&cnt[w], inc) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int x = mybin[k];
+        if (x > 0)
+            list[(long long)(x - 1) * M + nbase[x] + wc[x][k * 16 + w] + rank[k]] =
+                blockIdx.x * SCAN_ITEMS + k * 1024 + threadIdx.x;
     }
 }
 
-__global__ __launch_bounds__(1024) void k_scan_top(int nb, long long* __restrict__ part,
-                                                   Stats* __restrict__ stats) {
+// Symbolic bin lists from k_analyze's per-row bins (one light pass: k_analyze's
+// own grid is too fine-grained for per-block cursor atomics).
+__global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* __restrict__ bin_id,
+                                                   int* __restrict__ cnt, int* __restrict__ list) {
+    __shared__ unsigned char binof[SCAN_ITEMS];
+    for (int j = threadIdx.x; j < SCAN_ITEMS; j += 1024) {
+        const long long i = (long long)blockIdx.x * SCAN_ITEMS + j;
+        binof[j] = i < M ? bin_id[i] : 0;
+    }
+    __syncthreads();
+    append_block_rows<SYM_NB>(binof, M, cnt, list);
+}
+
+// Exclusive scan of the per-block partials (one block; run by the last reduce block).
+__device__ void scan_partials(int nb, long long* __restrict__ part, Stats* __restrict__ stats,
+                              const unsigned long long* __restrict__ blkflop, int nflop) {
+    {  // total products = sum of k_analyze's per-block partials
+        __shared__ unsigned long long fs[16];
+        unsigned long long f = 0;
+        for (int i = threadIdx.x; i < nflop; i += 1024) f += blkflop[i];
+        f = wave_sum(f);
+        if (lane_id() == 0) fs[threadIdx.x >> 6] = f;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long t = 0;
+            for (int k = 0; k < 16; ++k) t += fs[k];
+            stats->flop = t;
+        }
+    }
     __shared__ long long ws[16];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     long long carry = 0;
     for (int b = 0; b < nb; b += 1024) {
         const int i = b + threadIdx.x;
-        const long long x = i < nb ? part[i] : 0;
+        const long long x = i < nb ? __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
         const long long inc = wave_incl_scan64(x);
         if (lane == 63) ws[w] = inc;
         __syncthreads();
@@ -1235,14 +1192,35 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
 
 // Exclusive scan of the C row nnz (items [0, M], item M = 0 gives row_ptr[M])
 // plus the numeric bin of every row.
+__global__ __launch_bounds__(1024) void k_scan_reduce(int M, const int* __restrict__ Cptr,
+                                                      long long* __restrict__ part, Stats* __restrict__ stats,
+                                                      const unsigned long long* __restrict__ blkflop, int nflop) {
+    __shared__ long long ws[16];
+    const int base = blockIdx.x * SCAN_ITEMS;
+    long long s = 0;
+    for (int k = threadIdx.x; k < SCAN_ITEMS; k += 1024) {
+        const int i = base + k;
+        if (i < M) s += Cptr[i];
+    }
+    s = wave_sum(s);
+    if (lane_id() == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (int k = 0; k < 16; ++k) t += ws[k];
+        part[blockIdx.x] = t;
+    }
+    if (last_block_done(&stats->scan_done)) scan_partials(gridDim.x, part, stats, blkflop, nflop);
+}
+
 __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cptr,
                                                      const long long* __restrict__ part,
                                                      const int* __restrict__ rflop,
                                                      const int* __restrict__ rlo,
                                                      const int* __restrict__ rhi,
                                                      const int* __restrict__ ctiles,
-                                                     unsigned char* __restrict__ bin_id,
-                                                     Stats* __restrict__ stats, int dense_span_max) {
+                                                     int* __restrict__ list, Stats* __restrict__ stats,
+                                                     int dense_span_max, Published* pub, int seq) {
     constexpr int PER = SCAN_ITEMS / 1024;
     __shared__ long long ws[16];
     const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -1261,18 +1239,36 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
     long long off = part[blockIdx.x];
     for (int k = 0; k < w; ++k) off += ws[k];
     off += inc - loc;
+    __shared__ unsigned char nbin_of[SCAN_ITEMS];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = base + k;
         if (i <= M) Cptr[i] = (int)off;
+        int nbin = NUM_NONE;
         if (i < M) {
             const int n = v[k];
             const int lo = rlo[i], hi = rhi[i];
             const int span = n ? hi - lo + 1 : 0;
-            bin_id[i] = (unsigned char)num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need,
-                                                  dense_span_max);
+            nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max);
         }
+        nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
         off += v[k];
+    }
+    __syncthreads();
+    append_block_rows<NUM_NB>(nbin_of, M, stats->num_count, list);
+    if (!last_block_done(&stats->final_done)) return;
+    if (pub) {  // L1-bypassing reads, system-scope stores, release of the sequence number
+        constexpr int NW = (int)(sizeof(Stats) / 4);
+        static_assert(sizeof(Stats) % 4 == 0 && NW <= 1024, "Stats is copied one word per thread");
+        const int* src = reinterpret_cast<const int*>(stats);
+        int* dst = reinterpret_cast<int*>(&pub->stats);
+        if (threadIdx.x < NW)
+            __hip_atomic_store(dst + threadIdx.x,
+                               __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1291,7 +1287,7 @@ struct NumArgs {
     const int* rlo;
     const int* rhi;
     const int* ctiles;
-    const int* list;  // already offset to the bin's start
+    const int* list;  // the bin's rows (contiguous, row order within each scan block)
     int count;
     const int* Cptr;
     int* Ccol;
@@ -1505,12 +1501,25 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     }
 }
 
-int launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr) {
-    if (A.M <= 0) return 0;
-    const int G = pick_group(A.nnz, A.M);
-    const int rpb = 256 / G;
-    const dim3 grid((A.M + rpb - 1) / rpb), blk(256);
-#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.bin_id, Cptr, w.blkflop, w.stats)
+// k_analyze: G lanes per row, 256-thread blocks.
+static void analyze_geometry(long long nnzA, int M, int* G, int* blocks) {
+    *G = pick_group(nnzA, M);
+    const int rpb = 256 / *G;
+    *blocks = (M + rpb - 1) / rpb;
+}
+
+int analyze_blocks(long long nnzA, int M) {
+    int G, blocks;
+    analyze_geometry(nnzA, M, &G, &blocks);
+    return blocks;
+}
+
+void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr) {
+    if (A.M <= 0) return;
+    int G, blocks;
+    analyze_geometry(A.nnz, A.M, &G, &blocks);
+    const dim3 grid(blocks), blk(256);
+#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.stats)
     switch (G) {
     case 8: MHS_ANALYZE(8); break;
     case 16: MHS_ANALYZE(16); break;
@@ -1518,28 +1527,25 @@ int launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr
     default: MHS_ANALYZE(64); break;
     }
 #undef MHS_ANALYZE
-    return (int)grid.x;
+    hipLaunchKernelGGL(k_bin_list, dim3((A.M + SCAN_ITEMS - 1) / SCAN_ITEMS), dim3(1024), 0, s, A.M, w.sym_bin,
+                       w.stats->sym_count, w.bin_list);
 }
 
-void launch_binning(int M, const Work& w, int phase, hipStream_t s, int nflop_blocks, Published* pub, int seq) {
-    if (M <= 0) return;
-    const int nb = phase == 0 ? SYM_NB : NUM_NB;
-    const int nblk = (M + BIN_BLOCK - 1) / BIN_BLOCK;
-    hipLaunchKernelGGL(k_bin_count, dim3(nblk), dim3(BIN_BLOCK), 0, s, M, nb, nblk, w.bin_id, w.blkcnt);
-    int* cnt = phase == 0 ? w.stats->sym_count : w.stats->num_count;
-    long long* st = phase == 0 ? w.stats->sym_start : w.stats->num_start;
-    hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, nb, nblk, w.blkcnt, cnt, st, w.blkflop,
-                       phase == 0 ? nflop_blocks : 0, &w.stats->flop, w.stats, pub, seq);
-    hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(BIN_BLOCK), 0, s, M, nb, nblk, w.bin_id, w.blkcnt, w.rowlist);
-}
-
-void init_kernel_attributes() {
+hipError_t init_kernel_attributes() {
     // gfx950 grants up to 160 KiB of LDS per workgroup; make the large dynamic
-    // requests explicit for the block-per-row kernels.
-    (void)hipFuncSetAttribute((const void*)k_sym_block<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)k_num_block<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)k_num_block<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    // requests explicit for the block-per-row kernels (which use no static LDS).
+    hipError_t e = hipFuncSetAttribute((const void*)k_sym_block<1024, false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_num_block<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                LDS_MAX);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_num_block<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                LDS_MAX);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                LDS_MAX);
+    return e;
 }
 
 size_t sym_global_bytes_per_block(int N) {
@@ -1559,7 +1565,7 @@ void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipSt
     a.rtflop = w.rtflop;
     a.rlo = w.rlo;
     a.rhi = w.rhi;
-    a.list = w.rowlist;
+    a.list = w.bin_list;
     a.stats = w.stats;
     a.Cptr = Cptr;
     a.ctiles = w.ctiles;
@@ -1579,13 +1585,13 @@ void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipSt
     hipLaunchKernelGGL((k_sym_block<1024, true>), dim3(global_grid), dim3(1024), BLOCK_HDR, s, a);
 }
 
-void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max) {
+void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max, Published* pub,
+                          int seq) {
     const int nb = (M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS;
     long long* part = (long long*)w.scan_part;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(1024), 0, s, M, Cptr, part);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, nb, part, w.stats);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.stats, w.blkflop, w.nflop);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.rflop, w.rlo, w.rhi,
-                       w.ctiles, w.bin_id, w.stats, dense_span_max);
+                       w.ctiles, w.bin_list, w.stats, dense_span_max, pub, seq);
 }
 
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
@@ -1611,34 +1617,35 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
     a.Cval = Cval;
     a.gscratch = (char*)w.gscratch;
     a.gbytes = 0;
+
     // Largest bins first so the long rows start early.
     if (h.num_count[NUM_GLOBAL] > 0) {
-        a.list = w.rowlist + h.num_start[NUM_GLOBAL];
-        a.count = h.num_count[NUM_GLOBAL];
+        const int count = a.count = h.num_count[NUM_GLOBAL];
+        a.list = w.bin_list + (long long)(NUM_GLOBAL - 1) * A.M;
         a.gbytes = align16(h.num_global_need);
-        const int g = a.count < global_grid ? a.count : global_grid;
+        const int g = count < global_grid ? count : global_grid;
         hipLaunchKernelGGL((k_num_block<1024, true>), dim3(g), dim3(1024), BLOCK_HDR, s, a);
     }
     if (h.num_count[NUM_B1024] > 0) {
-        a.list = w.rowlist + h.num_start[NUM_B1024];
-        a.count = h.num_count[NUM_B1024];
-        hipLaunchKernelGGL((k_num_block<1024, false>), dim3(round8(a.count, 256)), dim3(1024), LDS_MAX - 1024, s, a);
+        const int count = a.count = h.num_count[NUM_B1024];
+        a.list = w.bin_list + (long long)(NUM_B1024 - 1) * A.M;
+        hipLaunchKernelGGL((k_num_block<1024, false>), dim3(round8(count, 256)), dim3(1024), LDS_MAX - 1024, s, a);
     }
     if (h.num_count[NUM_B256] > 0) {
-        a.list = w.rowlist + h.num_start[NUM_B256];
-        a.count = h.num_count[NUM_B256];
-        hipLaunchKernelGGL((k_num_block<256, false>), dim3(round8(a.count, 1024)), dim3(256), NUM_B256_BYTES, s, a);
+        const int count = a.count = h.num_count[NUM_B256];
+        a.list = w.bin_list + (long long)(NUM_B256 - 1) * A.M;
+        hipLaunchKernelGGL((k_num_block<256, false>), dim3(round8(count, 1024)), dim3(256), NUM_B256_BYTES, s, a);
     }
     if (h.num_count[NUM_W16] > 0) {
-        a.list = w.rowlist + h.num_start[NUM_W16];
-        a.count = h.num_count[NUM_W16];
-        hipLaunchKernelGGL(k_num_wave<NUM_W16_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, 2048)), dim3(256),
+        const int count = a.count = h.num_count[NUM_W16];
+        a.list = w.bin_list + (long long)(NUM_W16 - 1) * A.M;
+        hipLaunchKernelGGL(k_num_wave<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
                            WPB * NUM_W16_BYTES, s, a);
     }
     if (h.num_count[NUM_WS] > 0) {
-        a.list = w.rowlist + h.num_start[NUM_WS];
-        a.count = h.num_count[NUM_WS];
-        hipLaunchKernelGGL(k_num_wave<NUM_WS_BYTES>, dim3(round8((a.count + WPB - 1) / WPB, MHS_NUM_WS_GRID)), dim3(256),
+        const int count = a.count = h.num_count[NUM_WS];
+        a.list = w.bin_list + (long long)(NUM_WS - 1) * A.M;
+        hipLaunchKernelGGL(k_num_wave<NUM_WS_BYTES>, dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)), dim3(256),
                            WPB * NUM_WS_BYTES, s, a);
     }
 }

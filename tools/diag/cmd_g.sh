@@ -1,1 +1,1 @@
-for m in cant webbase-1M cop20k_A scircuit; do MATRIX=$m tools/diag/ab.sh "head||tools/diag/vHEAD" "rg32||tools/diag/vrg32" "rg32s||tools/diag/vrg32s" | sed "s/^/$m /" >> gpurun_out/ab_rgs.log 2>&1 || exit $?; done
+for m in cant cop20k_A webbase-1M; do MATRIX=$m tools/diag/ab.sh "head||tools/diag/vHEAD" "new||mh-spgemm_amd/mhspgemm" | sed "s/^/$m /" >> gpurun_out/ab_fuse.log 2>&1 || exit $?; done
