@@ -56,6 +56,15 @@
 #ifndef MHS_RUN_GMIN
 #define MHS_RUN_GMIN 32  // narrowest lane group of a chunk with merged runs
 #endif
+#ifndef MHS_MASK_GMAX
+#define MHS_MASK_GMAX 64
+#endif
+#ifndef MHS_AN_GMAX
+#define MHS_AN_GMAX 8  // k_analyze: 8 lanes per row (several rows per wave overlap their load chains)
+#endif
+#ifndef MHS_AN_UNROLL
+#define MHS_AN_UNROLL 1
+#endif
 #ifndef MHS_PIPE
 #define MHS_PIPE 0  // software-pipelined value walk
 #endif
@@ -474,6 +483,7 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
     int lo = INT_MAX, hi = -1, err = 0;
     if (valid) {
         const int s = Aptr[row], e = Aptr[row + 1];
+#pragma unroll MHS_AN_UNROLL
         for (int j = s + gl; j < e; j += G) {
             const int k = Acol[j];
             if (k < 0 || k >= MB) {
@@ -1475,10 +1485,10 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
 
 // -------------------------------------------------------------- launchers ---
 
-static int pick_group(long long nnz, int rows) {
+static int pick_group(long long nnz, int rows, int gmax = 64) {
     const long long avg = rows > 0 ? (nnz + rows - 1) / rows : 1;
     int g = 8;
-    while (g < avg && g < 64) g <<= 1;
+    while (g < avg && g < gmax) g <<= 1;
     return g;
 }
 
@@ -1490,7 +1500,11 @@ static int round8(long long x, int cap) {
 
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     if (B.M <= 0) return;
-    const int G = pick_group(B.nnz, B.M);
+    // about four chunk iterations per row: a wave then holds several rows, whose
+    // dependent load chains overlap (measured on gfx950: 64-lane rows were latency-bound)
+    const long long avg = B.M > 0 ? B.nnz / B.M : 0;
+    int G = 8;
+    while (2 * G <= avg / 4 && G < MHS_MASK_GMAX) G <<= 1;
     const int rpb = 256 / G;
     const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
     switch (G) {
@@ -1503,7 +1517,7 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
 
 // k_analyze: G lanes per row, 256-thread blocks.
 static void analyze_geometry(long long nnzA, int M, int* G, int* blocks) {
-    *G = pick_group(nnzA, M);
+    *G = pick_group(nnzA, M, MHS_AN_GMAX);
     const int rpb = 256 / *G;
     *blocks = (M + rpb - 1) / rpb;
 }

@@ -7,4 +7,4 @@ mkdir -p $1
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $2 -c $SRC/mhs_kernels.hip -o $1/k.o
 [ -f api.o ] || hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -x hip -c $SRC/mhs_api.cpp -o api.o
 [ -f mmio.o ] || hipcc -O3 -std=c++17 -fPIC -c $SRC/mhs_mmio.cpp -o mmio.o
-hipcc --offload-arch=gfx950 -shared -fPIC -o $1/libmhspgemm.so $1/k.o api.o mmio.o -lpthread
+hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined -o $1/libmhspgemm.so $1/k.o api.o mmio.o -lpthread
