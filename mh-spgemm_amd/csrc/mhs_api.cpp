@@ -39,7 +39,11 @@ struct mhs_ctx {
     Published* d_pub = nullptr;
     int seq = 0;
     hipEvent_t ev[8] = {};
-    bool sync = true;  // MHS_OPT_SYNC
+    hipStream_t side = nullptr;  // concurrent block-per-row symbolic bins
+    hipEvent_t fork = nullptr, join = nullptr;
+    bool sync = true;      // MHS_OPT_SYNC
+    bool use_side = false;  // MHS_SIDE_STREAM=1: block-per-row symbolic bins on a side stream (the
+                            // fork/join costs ~15 us on gfx950: pays only when those bins hold work)
     // MHS_OPT_NUMERIC_EVENTS: ring of (start, end) events around the numeric phase
     std::vector<hipEvent_t> nev;
     long long ncalls = 0;
@@ -219,6 +223,9 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (e == hipSuccess) memset(ctx->pub, 0, sizeof(Published));
     for (int i = 0; e == hipSuccess && i < 8; ++i) e = hipEventCreate(&ctx->ev[i]);
     if (e == hipSuccess) e = init_kernel_attributes();
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming);
     if (e != hipSuccess) {
         fprintf(stderr, "mhs_ctx_create: %s\n", hipGetErrorString(e));
         delete ctx;
@@ -227,6 +234,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     ctx->stream = ctx->own_stream;
     if (const char* e = getenv("MHS_DENSE_SPAN")) ctx->dense_span_max = atoi(e);
     if (getenv("MHS_NO_MCACHE")) ctx->use_mcache = false;
+    if (const char* e = getenv("MHS_SIDE_STREAM")) ctx->use_side = atoi(e) != 0;
     *out = ctx;
     return MHS_OK;
 }
@@ -244,6 +252,12 @@ void mhs_ctx_destroy(mhs_ctx* ctx) {
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    if (ctx->side) {
+        (void)hipStreamSynchronize(ctx->side);
+        (void)hipStreamDestroy(ctx->side);
+    }
+    if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+    if (ctx->join) (void)hipEventDestroy(ctx->join);
     delete ctx;
 }
 
@@ -354,7 +368,8 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     launch_analyze(a, w, MB, s, out.ptr);
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[2], s));
     // ---- Calculate_C_nnz ------------------------------------------------------------
-    launch_symbolic(a, w, M, N, out.ptr, s, sym_grid);
+    MHS_HIP(launch_symbolic(a, w, M, N, out.ptr, s, sym_grid, ctx->use_side ? ctx->side : nullptr, ctx->fork,
+                            ctx->join));
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
     Stats h;

@@ -186,8 +186,8 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);
 void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr);
 int analyze_blocks(long long nnzA, int M);
 
-void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s,
-                     int global_grid);
+hipError_t launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid,
+                           hipStream_t side = nullptr, hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
 void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max,
                           Published* pub, int seq);
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,

@@ -1567,8 +1567,9 @@ size_t sym_global_bytes_per_block(int N) {
     return (size_t)hash_slots(span_max) * 16;
 }
 
-void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid) {
-    if (M <= 0) return;
+hipError_t launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid,
+                           hipStream_t side, hipEvent_t fork, hipEvent_t join) {
+    if (M <= 0) return hipSuccess;
     SymArgs a;
     a.M = M;
     a.Aptr = A.ptr;
@@ -1587,16 +1588,31 @@ void launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipSt
     a.gbytes = (long long)sym_global_bytes_per_block(N);
     a.mcache = w.mcache;
     // Persistent grids: the bin sizes stay on the device (no host round trip);
-    // blocks past a bin's rows exit at once.
+    // blocks past a bin's rows exit at once.  The block-per-row bins run on the side
+    // stream, concurrently with the wave bin (rows are independent): their launches,
+    // empty or not, overlap the wave kernel instead of following it.
+    hipStream_t sb = s;
+    if (side) {
+        hipError_t e = hipEventRecord(fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+        if (e != hipSuccess) return e;
+        sb = side;
+    }
+    a.bin = SYM_GLOBAL;
+    hipLaunchKernelGGL((k_sym_block<1024, true>), dim3(global_grid), dim3(1024), BLOCK_HDR, sb, a);
+    a.bin = SYM_B1024;
+    hipLaunchKernelGGL((k_sym_block<1024, false>), dim3(round8(M, 256)), dim3(1024), LDS_MAX - 1024, sb, a);
+    a.bin = SYM_B256;
+    hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, 1024)), dim3(256), SYM_B256_BYTES, sb, a);
     a.bin = SYM_WAVE;
     hipLaunchKernelGGL(k_sym_wave<SYM_WAVE_BYTES>, dim3(round8((M + WPB - 1) / WPB, 2048)), dim3(256),
                        WPB * SYM_WAVE_BYTES, s, a);
-    a.bin = SYM_B256;
-    hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, 1024)), dim3(256), SYM_B256_BYTES, s, a);
-    a.bin = SYM_B1024;
-    hipLaunchKernelGGL((k_sym_block<1024, false>), dim3(round8(M, 256)), dim3(1024), LDS_MAX - 1024, s, a);
-    a.bin = SYM_GLOBAL;
-    hipLaunchKernelGGL((k_sym_block<1024, true>), dim3(global_grid), dim3(1024), BLOCK_HDR, s, a);
+    if (side) {
+        hipError_t e = hipEventRecord(join, side);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+        return e;
+    }
+    return hipSuccess;
 }
 
 void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max, Published* pub,
