@@ -42,6 +42,7 @@ struct mhs_ctx {
     hipStream_t side = nullptr;  // concurrent block-per-row symbolic bins
     hipEvent_t fork = nullptr, join = nullptr;
     bool sync = true;      // MHS_OPT_SYNC
+    bool groups = true;     // row groups (MHS_NO_GROUPS=1: every row alone)
     bool use_side = false;  // MHS_SIDE_STREAM=1: block-per-row symbolic bins on a side stream (the
                             // fork/join costs ~15 us on gfx950: pays only when those bins hold work)
     // MHS_OPT_NUMERIC_EVENTS: ring of (start, end) events around the numeric phase
@@ -144,7 +145,7 @@ void pool_put(mhs_ctx* ctx, void* p) {
 }
 
 struct Layout {
-    size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, bin_list, scan_part, mcache,
+    size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, asame, grp, bin_list, scan_part, mcache,
         stats, blkflop, total;
 };
 
@@ -168,6 +169,8 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB) {
     L.rhi = take((size_t)M * 4);
     L.ctiles = take((size_t)M * 4);
     L.sym_bin = take((size_t)M);
+    L.asame = take((size_t)M);
+    L.grp = take((size_t)M);
     static_assert((int)NUM_NB >= (int)SYM_NB, "bin_list holds either phase's bins");
     L.bin_list = take((size_t)(NUM_NB - 1) * M * 4);
     L.blkflop = take(((size_t)analyze_blocks(nnzA, M) + 1) * 8);
@@ -235,6 +238,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_DENSE_SPAN")) ctx->dense_span_max = atoi(e);
     if (getenv("MHS_NO_MCACHE")) ctx->use_mcache = false;
     if (const char* e = getenv("MHS_SIDE_STREAM")) ctx->use_side = atoi(e) != 0;
+    if (getenv("MHS_NO_GROUPS")) ctx->groups = false;
     *out = ctx;
     return MHS_OK;
 }
@@ -343,6 +347,9 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     w.rhi = (int*)(ctx->ws + L.rhi);
     w.ctiles = (int*)(ctx->ws + L.ctiles);
     w.sym_bin = (unsigned char*)(ctx->ws + L.sym_bin);
+    w.asame = (unsigned char*)(ctx->ws + L.asame);
+    w.grp = (unsigned char*)(ctx->ws + L.grp);
+    w.groups = ctx->groups ? 1 : 0;
     w.bin_list = (int*)(ctx->ws + L.bin_list);
     w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
     w.nflop = M > 0 ? analyze_blocks(A->nnz, M) : 0;

@@ -31,9 +31,18 @@ constexpr int SCAN_ITEMS = 4096;// rows per block in the row_ptr scan
 // Symbolic bins (by LDS need and tile work).
 enum SymBin : int { SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_NB = 5 };
 // Numeric bins (by LDS need and product work).
+// NUM_WSG / NUM_W16G: row groups (up to RG_MAX consecutive rows of A with one
+// column pattern, processed together by one wave: every B value loaded feeds R rows).
 enum NumBin : int {
-    NUM_NONE = 0, NUM_WS = 1, NUM_W16 = 2, NUM_B256 = 3, NUM_B1024 = 4, NUM_GLOBAL = 5, NUM_NB = 6
+    NUM_NONE = 0, NUM_WS = 1, NUM_W16 = 2, NUM_B256 = 3, NUM_B1024 = 4, NUM_GLOBAL = 5, NUM_WSG = 6,
+    NUM_W16G = 7, NUM_NB = 8
 };
+// Row groups: rows i-1, i of A with the same column pattern (FEM dofs of one node)
+// have C rows with one pattern.  Maximal runs are broken every RG_BREAK rows and cut
+// into groups of at most RG_MAX rows; grp[head] = R, grp[head + o] = GRP_CONT | o.
+constexpr int RG_MAX = 3;
+constexpr int RG_BREAK = 96;  // a multiple of 2, 3, 4 and 6: dof blocks of those sizes stay whole
+constexpr int GRP_CONT = 0x80;
 
 // Per-team LDS budgets (bytes).  The wave kernels carve one region per wave.
 constexpr int SYM_WAVE_BYTES = 4096;
@@ -44,6 +53,7 @@ constexpr int NUM_WS_BYTES = 5120;   // 4 waves x 5 KiB = 20 KiB/block: 8 blocks
 constexpr int NUM_WS_WORK = 8192;       // products a single wave takes on
 constexpr int NUM_W16_BYTES = 16384;
 constexpr int NUM_W16_WORK = 32768;
+constexpr int NUM_WSG_BYTES = 10240;  // grouped rows: 4 waves x 10 KiB = 40 KiB/block (4 per CU)
 constexpr int NUM_B256_BYTES = 65536;
 constexpr int NUM_B256_WORK = 1 << 22;
 constexpr int LDS_MAX = 163840;         // gfx950: 160 KiB per workgroup (probed on the box)
@@ -150,6 +160,20 @@ __host__ __device__ inline long long num_need(int span, int t, int n, int dense_
     return m == NM_DENSE ? num_need_dense(span) : m == NM_RMAP ? num_need_rmap(span, n)
                                                : m == NM_DIRECT ? num_need_direct(span, n) : num_need_hash(t, n);
 }
+// One row's accumulator bytes in mode m (16-aligned); a group of R rows needs the
+// tables once and R accumulators.
+__host__ __device__ inline long long num_acc_bytes(int m, int span, int t, int n) {
+    if (m == NM_DENSE) return (long long)span * 64 * 8;
+    if (m == NM_HASH) {
+        const int p = next_pow2(t);
+        return align16((long long)(n > p ? n : p) * 8);
+    }
+    return align16((long long)n * 8);
+}
+__host__ __device__ inline long long num_need_rows(int span, int t, int n, int dense_span_max, int R) {
+    const int m = num_mode(span, t, n, dense_span_max);
+    return num_need(span, t, n, dense_span_max) + (long long)(R - 1) * num_acc_bytes(m, span, t, n);
+}
 
 // ------------------------------------------------------------ launchers ---
 struct Csr {
@@ -172,6 +196,9 @@ struct Work {
     int* rhi;
     int* ctiles;
     unsigned char* sym_bin;  // M: symbolic bin of every row (k_analyze)
+    unsigned char* asame;    // M: row has the column pattern of row-1 (k_analyze)
+    unsigned char* grp;      // M: row groups (k_bin_list; see RG_MAX)
+    int groups;              // form row groups (0: every row alone)
     int* bin_list;           // (NUM_NB-1) * M: bin x's rows at (x-1)*M (symbolic bins, then numeric bins)
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count

@@ -474,6 +474,7 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
                                                  int* __restrict__ rhi, int* __restrict__ ctiles,
                                                  unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
                                                  unsigned long long* __restrict__ blkflop,
+                                                 unsigned char* __restrict__ asame,
                                                  Stats* __restrict__ stats) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
@@ -481,11 +482,17 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
     const bool valid = row < M;
     long long flop = 0, tflop = 0;
     int lo = INT_MAX, hi = -1, err = 0;
+    bool differ = true;  // row's column pattern differs from row-1's (row groups)
     if (valid) {
         const int s = Aptr[row], e = Aptr[row + 1];
+        const int ps = row > 0 ? Aptr[row - 1] : 0;
+        differ = !(row > 0 && e > s && s - ps == e - s);
+        const int dp = s - ps;
 #pragma unroll MHS_AN_UNROLL
         for (int j = s + gl; j < e; j += G) {
             const int k = Acol[j];
+            const int kp = Acol[j - dp];  // unconditional: stays in [0, nnz(A)); a guarded load would serialise
+            differ = differ || kp != k;
             if (k < 0 || k >= MB) {
                 err = ERR_ACOL_RANGE;
                 continue;
@@ -503,7 +510,13 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
         tflop += __shfl_xor(tflop, d);
         lo = min(lo, __shfl_xor(lo, d));
         hi = max(hi, __shfl_xor(hi, d));
+        const int od = __shfl_xor((int)differ, d);  // every lane shuffles (no short circuit)
+        differ = differ || od != 0;
     }
+    if (valid && gl == 0) asame[row] = (unsigned char)(differ ? 0 : 1);
+#ifdef MHS_DEBUG_PRINT
+    if (valid && M < 16) printf("row %d gl %d differ %d\n", row, gl, (int)differ);
+#endif
     if (valid && gl == 0) {
         const int f = sat_int(flop), tf = sat_int(tflop);
         const int span = f ? hi - lo + 1 : 0;
@@ -643,6 +656,33 @@ __device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl
     }
 }
 
+// Row group: the same walk feeding RM (compile-time bound) accumulators, R of them
+// live: B entry q contributes sum_i a[r][i] * b_i to C row r.  One load per B row of
+// the run serves all R rows.
+template <int LM, int RM, class F>
+__device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int gl, int G,
+                                                  const double (&a)[RM][LM], int L, int R, int stride) {
+    int o[LM];
+#pragma unroll
+    for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
+    for (int q = gl; q < n; q += G) {
+        const int c = f.col(s + q);
+        double b[LM];
+#pragma unroll
+        for (int i = 0; i < LM; ++i) b[i] = f.val(s + o[i] + q);
+#pragma unroll
+        for (int i = 1; i < LM; ++i) pin(b[i]);
+        double v[RM];
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+            v[r] = a[r][0] * b[0];
+#pragma unroll
+            for (int i = 1; i < LM; ++i) v[r] += i < L ? a[r][i] * b[i] : 0.0;
+        }
+        f.add_rows(c, v, R, stride);
+    }
+}
+
 template <class F>
 __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
                                              const int* __restrict__ Acol,
@@ -686,6 +726,52 @@ __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
                 }
             } else {
                 run_segment(f, s, n, gl, G, 0.0);
+            }
+        }
+    }
+}
+
+// Row group (wave teams only): the head row's A entries are staged as usual and lane
+// j also holds the a-values of rows head+1 .. head+R-1 (rows of one pattern are
+// consecutive and equally long in A: entry j of row head+r sits at j + r*nA).
+template <class F>
+__device__ __forceinline__ void for_products_group(int a0, int a1, const int* __restrict__ Acol,
+                                                   const double* __restrict__ Aval,
+                                                   const int4* __restrict__ bmeta, int Grow, const F& f,
+                                                   int R, int nA, int stride) {
+    constexpr int RM = RG_MAX;
+    static_assert(MHS_RUN_MAX <= 3, "grouped walks merge runs of up to 3 B rows");
+    const int lane = lane_id();
+    for (int jb = a0; jb < a1; jb += 64) {
+        const StagedChunk x = stage_chunk(lane, jb, a1, Acol, Aval, bmeta, false);
+        const int jl = jb + lane;
+        double avr[RM];
+        avr[0] = x.av;
+#pragma unroll
+        for (int r = 1; r < RM; ++r) avr[r] = (jl < a1 && r < R) ? Aval[jl + r * nA] : 0.0;
+        const int G = (x.lmax > 1 && Grow < MHS_RUN_GMIN) ? MHS_RUN_GMIN : Grow;
+        const int gs = 31 - __clz(G);
+        const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
+        const int iters = (x.nh + ngrp - 1) / ngrp;
+        for (int it = 0; it < iters; ++it) {
+            const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
+            const int h = __shfl(x.src, e & 63);
+            const int sb = __shfl(x.st, h);
+            const int n0 = __shfl(x.ln, h);
+            const int n = e < x.nh ? n0 : 0;
+            const int L = __shfl(x.L, h);
+            if (x.lmax == 1) {
+                double a[RM][1];
+#pragma unroll
+                for (int r = 0; r < RM; ++r) a[r][0] = __shfl(avr[r], h);
+                run_segment_group<1, RM>(f, sb, n, gl, G, a, 1, R, stride);
+            } else {
+                double a[RM][3];
+#pragma unroll
+                for (int r = 0; r < RM; ++r)
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h + i, 63));
+                run_segment_group<3, RM>(f, sb, n, gl, G, a, L, R, stride);
             }
         }
     }
@@ -960,7 +1046,23 @@ struct Accum {
         asm volatile("" ::"v"(c), "v"(v));
         return;
 #endif
-        const Item x{c, v};
+        const int idx = index(c);
+#if MHS_NUM_DIAG == 1  // diagnostic build: plain LDS store instead of the atomic add
+        acc[idx] = v;
+#else
+        acc_add<GM>(&acc[idx], v);
+#endif
+    }
+    // row group: accumulator slice r (stride `stride` doubles) of column c += v[r], r < R
+    template <int RM>
+    __device__ __forceinline__ void add_rows(int c, const double (&v)[RM], int R, int stride) const {
+        const int idx = index(c);
+#pragma unroll
+        for (int r = 0; r < RM; ++r)
+            if (r < R) acc_add<GM>(&acc[idx + r * stride], v[r]);
+    }
+    __device__ __forceinline__ int index(int c) const {
+        const Item x{c, 0.0};
         int idx;
         if constexpr (MODE == NM_DENSE) {
             idx = x.c - colbase;
@@ -980,11 +1082,7 @@ struct Accum {
             const unsigned long long below = (1ull << (x.c & (TILE_BITS - 1))) - 1;
             idx = (int)q.z + __popcll(mask & below);
         }
-#if MHS_NUM_DIAG == 1  // diagnostic build: plain LDS store instead of the atomic add
-        acc[idx] = v;
-#else
-        acc_add<GM>(&acc[idx], v);
-#endif
+        return idx;
     }
 };
 
@@ -1024,6 +1122,7 @@ struct SymArgs {
     const int* rhi;
     const int* list;  // bin x's rows at list + (x-1)*M, count in stats->sym_count[x]
     const Stats* stats;
+    const unsigned char* grp;  // row groups: R of every listed head
     int bin;
     int* Cptr;
     int* ctiles;
@@ -1056,14 +1155,17 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
     }
     n = tm.sum(n);
     t = tm.sum(t);
-    if (tm.rank() == 0) {
-        a.Cptr[row] = (int)n;
-        a.ctiles[row] = t;
+    const int R = __builtin_amdgcn_readfirstlane((int)a.grp[row]);  // the group's rows share the pattern
+    if (tm.rank() < R) {
+        a.Cptr[row + tm.rank()] = (int)n;
+        a.ctiles[row + tm.rank()] = t;
     }
     // numeric reuses the OR'd masks of narrow rows (span <= 32 < team size: one store per lane)
     const int r_ = tm.rank();
-    if (direct && span <= MCACHE_SPAN && r_ < span && a.mcache)
-        a.mcache[(size_t)row * MCACHE_SPAN + r_] = E[r_].mask;
+    if (direct && span <= MCACHE_SPAN && r_ < span && a.mcache) {
+        const unsigned long long m = E[r_].mask;
+        for (int g = 0; g < R; ++g) a.mcache[(size_t)(row + g) * MCACHE_SPAN + r_] = m;
+    }
     tm.sync();
 }
 
@@ -1134,14 +1236,35 @@ __device__ void append_block_rows(const unsigned char* binof, long long M, int* 
     }
 }
 
-// Symbolic bin lists from k_analyze's per-row bins (one light pass: k_analyze's
-// own grid is too fine-grained for per-block cursor atomics).
+// Row groups and the symbolic bin lists (one light pass after k_analyze, whose grid
+// is too fine-grained for per-block cursor atomics).  Row i's group: the maximal run
+// of same-pattern rows containing it, broken every RG_BREAK rows, cut into groups of
+// RG_MAX from the run start.  Only group heads enter the symbolic lists (a group's
+// rows share one C pattern).
 __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* __restrict__ bin_id,
+                                                   const unsigned char* __restrict__ asame,
+                                                   unsigned char* __restrict__ grp, int groups,
                                                    int* __restrict__ cnt, int* __restrict__ list) {
     __shared__ unsigned char binof[SCAN_ITEMS];
     for (int j = threadIdx.x; j < SCAN_ITEMS; j += 1024) {
         const long long i = (long long)blockIdx.x * SCAN_ITEMS + j;
-        binof[j] = i < M ? bin_id[i] : 0;
+        unsigned char b = 0;
+        if (i < M) {
+            int g = 1;
+            if (groups && asame[i]) {
+                long long rs = i;
+                const long long lim = i - i % RG_BREAK;
+                while (rs > lim && asame[rs]) --rs;
+                const int o = (int)((i - rs) % RG_MAX);
+                if (o) g = GRP_CONT | o;
+            }
+            if (groups && g == 1) {  // a head: count the rows that follow it in its group
+                while (g < RG_MAX && i + g < M && (i + g) % RG_BREAK != 0 && asame[i + g]) ++g;
+            }
+            grp[i] = (unsigned char)g;
+            b = (g & GRP_CONT) ? 0 : bin_id[i];
+        }
+        binof[j] = b;
     }
     __syncthreads();
     append_block_rows<SYM_NB>(binof, M, cnt, list);
@@ -1200,6 +1323,15 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
     return NUM_GLOBAL;
 }
 
+// Grouped numeric bin of a group of R rows (NUM_NONE: run its rows one by one).
+__device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t, int R, int dense_span_max) {
+    if (R < 2 || n == 0) return NUM_NONE;
+    const long long need = num_need_rows(span, t, n, dense_span_max, R);
+    if (need <= NUM_WSG_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WSG;
+    if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16G;
+    return NUM_NONE;
+}
+
 // Exclusive scan of the C row nnz (items [0, M], item M = 0 gives row_ptr[M])
 // plus the numeric bin of every row.
 __global__ __launch_bounds__(1024) void k_scan_reduce(int M, const int* __restrict__ Cptr,
@@ -1229,6 +1361,7 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
                                                      const int* __restrict__ rlo,
                                                      const int* __restrict__ rhi,
                                                      const int* __restrict__ ctiles,
+                                                     const unsigned char* __restrict__ grp,
                                                      int* __restrict__ list, Stats* __restrict__ stats,
                                                      int dense_span_max, Published* pub, int seq) {
     constexpr int PER = SCAN_ITEMS / 1024;
@@ -1259,7 +1392,15 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
             const int n = v[k];
             const int lo = rlo[i], hi = rhi[i];
             const int span = n ? hi - lo + 1 : 0;
-            nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max);
+            const int g = grp[i];
+            // a group runs as one item when its R accumulators fit a wave bin; its
+            // members decide alike (same pattern, same sizes) and then stay out
+            const int gh = (g & GRP_CONT) ? grp[i - (g & 0x7F)] : g;
+            const int gb = num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max);
+            if (gb != NUM_NONE)
+                nbin = (g & GRP_CONT) ? NUM_NONE : gb;
+            else
+                nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max);
         }
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
         off += v[k];
@@ -1299,6 +1440,7 @@ struct NumArgs {
     const int* ctiles;
     const int* list;  // the bin's rows (contiguous, row order within each scan block)
     int count;
+    const unsigned char* grp;  // row groups (grouped bins: R of every head)
     const int* Cptr;
     int* Ccol;
     double* Cval;
@@ -1308,10 +1450,10 @@ struct NumArgs {
     const unsigned long long* mcache;
 };
 
-template <class Team, bool GLOBALMEM, int MODE>
+template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
 __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, int span, int t,
                              int c0, int n, int a0, int a1, char* region, int* counter,
-                             int4* stage) {
+                             int4* stage, int R) {
     MHS_STAMP0();
     const int H = MODE == NM_HASH ? hash_slots(t) : span;
     const int hshift = MODE == NM_HASH ? ilog2(H) : 0;
@@ -1322,6 +1464,9 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                             (MODE == NM_RMAP ? align16((long long)span * TILE_BITS * 2) : 0));
     const int nacc = MODE == NM_DENSE ? span * TILE_BITS : n;
     const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
+    // row group: R accumulator slices `stride` doubles apart; C row r at c0 + r*n
+    const int stride = GROUPED ? (int)(num_acc_bytes(MODE, span, t, n) / 8) : 0;
+    const int nclear = GROUPED ? (R - 1) * stride + nacc : nacc;
 
     // 1. the C row's tile table: the symbolic pass's masks when it kept them,
     //    else rebuilt (same OR pass as symbolic)
@@ -1380,14 +1525,18 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
         tm.sync();
     }
     MHS_STAMP(2);
-    for (int r = tm.rank(); r < nacc; r += Team::size) acc[r] = 0.0;
+    for (int r = tm.rank(); r < nclear; r += Team::size) acc[r] = 0.0;
     tm.sync();
     MHS_STAMP(3);
 
-    // 3. accumulate every product of the row
+    // 3. accumulate every product of the row (of the group's rows)
     {
         const Accum<GLOBALMEM, MODE> f{E, acc, rmap, lo, H, hshift, colbase, a.Bcol, a.Bval};
-        walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
+        if constexpr (GROUPED)
+            for_products_group(a0, a1, a.Acol, a.Aval, a.bmeta, pick_group(a.rflop[row], a1 - a0, 64), f, R,
+                               a1 - a0, stride);
+        else
+            walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
     }
     tm.sync();
     MHS_STAMP(4);
@@ -1401,12 +1550,15 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             const TileEntry e = E[s];
             if ((e.mask >> lane) & 1ull) {
                 const int pos = c0 + e.base + __popcll(e.mask & lanemask_lt());
-                a.Ccol[pos] = colbase + (s << TILE_SHIFT) + lane;
-                a.Cval[pos] = acc[(s << TILE_SHIFT) + lane];
+                for (int g = 0; g < (GROUPED ? R : 1); ++g) {
+                    a.Ccol[pos + g * n] = colbase + (s << TILE_SHIFT) + lane;
+                    a.Cval[pos + g * n] = acc[g * stride + (s << TILE_SHIFT) + lane];
+                }
             }
         }
     } else {
-        for (int r = tm.rank(); r < n; r += Team::size) a.Cval[c0 + r] = acc[r];
+        for (int g = 0; g < (GROUPED ? R : 1); ++g)
+            for (int r = tm.rank(); r < n; r += Team::size) a.Cval[c0 + g * n + r] = acc[g * stride + r];
         if (n >= 8 * t) {
             // dense masks: one wave per tile, lane = bit
             const int lane = lane_id();
@@ -1414,8 +1566,10 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             for (int s = wv; s < H; s += nw) {
                 const TileEntry e = E[s];
                 const int key = MODE != NM_HASH ? lo + s : e.key;
-                if (e.mask && ((e.mask >> lane) & 1ull))
-                    a.Ccol[c0 + e.base + __popcll(e.mask & lanemask_lt())] = (key << TILE_SHIFT) + lane;
+                if (e.mask && ((e.mask >> lane) & 1ull)) {
+                    const int pos = c0 + e.base + __popcll(e.mask & lanemask_lt());
+                    for (int g = 0; g < (GROUPED ? R : 1); ++g) a.Ccol[pos + g * n] = (key << TILE_SHIFT) + lane;
+                }
             }
         } else {
             for (int s = tm.rank(); s < H; s += Team::size) {
@@ -1426,7 +1580,8 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                 int r = c0 + e.base;
                 while (mk) {
                     const int b = __builtin_ctzll(mk);
-                    a.Ccol[r++] = (key << TILE_SHIFT) + b;
+                    for (int g = 0; g < (GROUPED ? R : 1); ++g) a.Ccol[r + g * n] = (key << TILE_SHIFT) + b;
+                    ++r;
                     mk &= mk - 1;
                 }
             }
@@ -1438,9 +1593,9 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
 
 // Row-level scalars are made provably wave-uniform (readfirstlane) so that the
 // mode dispatch and every per-row loop bound compile to scalar control flow.
-template <class Team, bool GLOBALMEM>
+template <class Team, bool GLOBALMEM, bool GROUPED = false>
 __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region, int* counter,
-                        int4* stage) {
+                        int4* stage, int R = 1) {
     const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
     const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
     const int span = hi - lo + 1;
@@ -1451,24 +1606,29 @@ __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region,
     const int a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
     const int mode = num_mode(span, t, n, a.dense_span_max);
     if (mode == NM_DENSE)
-        num_row_body<Team, GLOBALMEM, NM_DENSE>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
+        num_row_body<Team, GLOBALMEM, NM_DENSE, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else if (mode == NM_RMAP)
-        num_row_body<Team, GLOBALMEM, NM_RMAP>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
+        num_row_body<Team, GLOBALMEM, NM_RMAP, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else if (mode == NM_DIRECT)
-        num_row_body<Team, GLOBALMEM, NM_DIRECT>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
+        num_row_body<Team, GLOBALMEM, NM_DIRECT, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else
-        num_row_body<Team, GLOBALMEM, NM_HASH>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage);
+        num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
 }
 
-template <int BYTES>
+template <int BYTES, bool GROUPED = false>
 __global__ __launch_bounds__(256, MHS_NUM_WAVES_EU) void k_num_wave(NumArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int w = threadIdx.x >> 6;
     char* reg = smem + w * BYTES;
     WaveTeam tm;
-    for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride)
-        num_row<WaveTeam, false>(tm, a, __builtin_amdgcn_readfirstlane(a.list[rw.first]), reg + WAVE_HDR,
-                                 (int*)reg, nullptr);
+    for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride) {
+        const int row = __builtin_amdgcn_readfirstlane(a.list[rw.first]);
+        if constexpr (GROUPED)  // a group head: R rows of one pattern
+            num_row<WaveTeam, false, true>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
+                                           __builtin_amdgcn_readfirstlane((int)a.grp[row]));
+        else
+            num_row<WaveTeam, false>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr);
+    }
 }
 
 template <int T, bool GLOBALMEM>
@@ -1533,7 +1693,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.stats)
+#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats)
     switch (G) {
     case 8: MHS_ANALYZE(8); break;
     case 16: MHS_ANALYZE(16); break;
@@ -1542,7 +1702,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     }
 #undef MHS_ANALYZE
     hipLaunchKernelGGL(k_bin_list, dim3((A.M + SCAN_ITEMS - 1) / SCAN_ITEMS), dim3(1024), 0, s, A.M, w.sym_bin,
-                       w.stats->sym_count, w.bin_list);
+                       w.asame, w.grp, w.groups, w.stats->sym_count, w.bin_list);
 }
 
 hipError_t init_kernel_attributes() {
@@ -1559,6 +1719,9 @@ hipError_t init_kernel_attributes() {
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 LDS_MAX);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     return e;
 }
 
@@ -1582,6 +1745,7 @@ hipError_t launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr,
     a.rhi = w.rhi;
     a.list = w.bin_list;
     a.stats = w.stats;
+    a.grp = w.grp;
     a.Cptr = Cptr;
     a.ctiles = w.ctiles;
     a.gscratch = (char*)w.gscratch;
@@ -1621,7 +1785,7 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int de
     long long* part = (long long*)w.scan_part;
     hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.stats, w.blkflop, w.nflop);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.rflop, w.rlo, w.rhi,
-                       w.ctiles, w.bin_list, w.stats, dense_span_max, pub, seq);
+                       w.ctiles, w.grp, w.bin_list, w.stats, dense_span_max, pub, seq);
 }
 
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
@@ -1647,6 +1811,7 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
     a.Cval = Cval;
     a.gscratch = (char*)w.gscratch;
     a.gbytes = 0;
+    a.grp = w.grp;
 
     // Largest bins first so the long rows start early.
     if (h.num_count[NUM_GLOBAL] > 0) {
@@ -1671,6 +1836,18 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
         a.list = w.bin_list + (long long)(NUM_W16 - 1) * A.M;
         hipLaunchKernelGGL(k_num_wave<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
                            WPB * NUM_W16_BYTES, s, a);
+    }
+    if (h.num_count[NUM_W16G] > 0) {
+        const int count = a.count = h.num_count[NUM_W16G];
+        a.list = w.bin_list + (long long)(NUM_W16G - 1) * A.M;
+        hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true>), dim3(round8((count + WPB - 1) / WPB, 2048)),
+                           dim3(256), WPB * NUM_W16_BYTES, s, a);
+    }
+    if (h.num_count[NUM_WSG] > 0) {
+        const int count = a.count = h.num_count[NUM_WSG];
+        a.list = w.bin_list + (long long)(NUM_WSG - 1) * A.M;
+        hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
+                           dim3(256), WPB * NUM_WSG_BYTES, s, a);
     }
     if (h.num_count[NUM_WS] > 0) {
         const int count = a.count = h.num_count[NUM_WS];

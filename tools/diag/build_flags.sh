@@ -5,6 +5,6 @@ cd "$(dirname "$0")"
 SRC=../../mh-spgemm_amd/csrc
 mkdir -p $1
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $2 -c $SRC/mhs_kernels.hip -o $1/k.o
-[ -f api.o ] || hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -x hip -c $SRC/mhs_api.cpp -o api.o
-[ -f mmio.o ] || hipcc -O3 -std=c++17 -fPIC -c $SRC/mhs_mmio.cpp -o mmio.o
+[ api.o -nt $SRC/mhs_api.cpp ] && [ api.o -nt $SRC/mhs_internal.hpp ] || hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -x hip -c $SRC/mhs_api.cpp -o api.o
+[ mmio.o -nt $SRC/mhs_mmio.cpp ] || hipcc -O3 -std=c++17 -fPIC -c $SRC/mhs_mmio.cpp -o mmio.o
 hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined -o $1/libmhspgemm.so $1/k.o api.o mmio.o -lpthread
