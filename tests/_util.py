@@ -146,3 +146,34 @@ def run_zoo(seed: int = 5, N: int = 40_000):
     Acol = np.array([k for r in arows for k in r], np.int32)
     Av = rng.uniform(0.1, 1.0, len(Acol))
     return (M, K, Aptr.astype(np.int32), Acol, Av), (K, N, Bptr.astype(np.int32), Bc, Bv)
+
+
+def group_zoo(seed: int = 3, K: int = 6000, N: int = 30_000):
+    """A whose rows repeat column patterns (runs of 1..8 equal rows, so row groups of
+    1..3 and runs cut by the group size and by the 96-row breaks), with small,
+    medium and large patterns (grouped wave bins, the 16 KiB grouped bin, and
+    groups too large for any grouped bin that run row by row); B random (K x N)
+    with some same-pattern row runs of its own.  Values differ per row."""
+    rng = np.random.default_rng(seed)
+    arows = []
+    while len(arows) < 700:
+        size = int(rng.choice([2, 6, 20, 60, 200]))
+        pat = np.unique(rng.integers(0, K, size))
+        arows.extend([pat] * int(rng.integers(1, 9)))
+        if rng.random() < 0.1:
+            arows.append(np.zeros(0, np.int64))  # an empty row breaks a run
+    M = len(arows)
+    Aptr = np.zeros(M + 1, np.int64)
+    Aptr[1:] = np.cumsum([len(r) for r in arows])
+    Acol = np.concatenate(arows).astype(np.int32)
+    Av = rng.uniform(0.1, 1.0, len(Acol))
+    brows = []
+    while len(brows) < K:
+        pat = np.unique(rng.integers(0, N, int(rng.integers(1, 40))))
+        brows.extend([pat] * int(rng.integers(1, 4)))
+    brows = brows[:K]
+    Bptr = np.zeros(K + 1, np.int64)
+    Bptr[1:] = np.cumsum([len(r) for r in brows])
+    Bc = np.concatenate(brows).astype(np.int32)
+    Bv = rng.uniform(0.1, 1.0, len(Bc))
+    return (M, K, Aptr.astype(np.int32), Acol, Av), (K, N, Bptr.astype(np.int32), Bc, Bv)

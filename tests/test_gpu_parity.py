@@ -12,7 +12,7 @@ import pytest
 import mhspgemm
 from mhspgemm import synth
 from oracle import oracle as orc
-from _util import GOLDEN, PRODUCT_CASES, bin_zoo, load_golden, random_csr, run_zoo
+from _util import GOLDEN, PRODUCT_CASES, bin_zoo, group_zoo, load_golden, random_csr, run_zoo
 
 pytestmark = pytest.mark.gpu
 
@@ -100,9 +100,32 @@ def test_run_zoo_same_pattern_rows(tool, seed):
     assert t.num_bins[1] > 0 and t.num_bins[3] > 0, t.num_bins  # wave and block kernels saw rows
 
 
+@pytest.mark.parametrize("seed", [3, 4])
+def test_group_zoo_row_groups(tool, seed):
+    (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = group_zoo(seed)
+    A = mhspgemm.CSR(M, K, Ap, Ac, Av)
+    B = mhspgemm.CSR(K2, N, Bp, Bc, Bv)
+    t = check(tool, A, B)
+    assert t.num_bins[6] > 0, t.num_bins  # grouped wave bin used
+
+
+def test_row_groups_off_matches(tool, monkeypatch):
+    # the same product with row groups disabled (MHS_NO_GROUPS, read at context creation)
+    (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = group_zoo(5)
+    A = mhspgemm.CSR(M, K, Ap, Ac, Av)
+    B = mhspgemm.CSR(K2, N, Bp, Bc, Bv)
+    monkeypatch.setenv("MHS_NO_GROUPS", "1")
+    plain = mhspgemm.Tool(tool.device)
+    try:
+        t = check(plain, A, B)
+        assert t.num_bins[6] == 0 and t.num_bins[7] == 0, t.num_bins
+    finally:
+        plain.close()
+
+
 def test_fem_dof_runs_square(tool):
     # A*A with dof 1..4 per node: runs of every length up to and past the merge cap
-    for dof in (1, 2, 3, 4):
+    for dof in (1, 2, 3, 4, 6):
         A = synth.fem_grid(5, 4, 9, dof=dof)
         check(tool, A, A)
 
