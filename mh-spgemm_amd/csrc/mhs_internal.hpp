@@ -26,7 +26,7 @@ constexpr int TILE_SHIFT = 6;  // 64-column tiles, one uint64 mask each (wave64 
 constexpr int TILE_BITS = 64;
 constexpr int NBINS = 8;
 constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
-constexpr int SCAN_ITEMS = 4096;// rows per block in the row_ptr scan
+constexpr int SCAN_ITEMS = 1024;// rows per block in the row_ptr scan and the bin-list passes
 
 // Symbolic bins (by LDS need and tile work).
 enum SymBin : int { SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_NB = 5 };

@@ -65,6 +65,9 @@
 #ifndef MHS_AN_UNROLL
 #define MHS_AN_UNROLL 1
 #endif
+#ifndef MHS_GRP_UNROLL
+#define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
+#endif
 #ifndef MHS_PIPE
 #define MHS_PIPE 0  // software-pipelined value walk
 #endif
@@ -659,27 +662,46 @@ __device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl
 // Row group: the same walk feeding RM (compile-time bound) accumulators, R of them
 // live: B entry q contributes sum_i a[r][i] * b_i to C row r.  One load per B row of
 // the run serves all R rows.
-template <int LM, int RM, class F>
+template <int LM, int RM, bool FULL, class F>
 __device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int gl, int G,
                                                   const double (&a)[RM][LM], int L, int R, int stride) {
+    // U entries per lane issued together: a group's wave is latency-bound on these
+    // loads, and the grouped kernels' occupancy is set by LDS (registers to spare)
+    constexpr int U = MHS_GRP_UNROLL;
     int o[LM];
 #pragma unroll
     for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
-    for (int q = gl; q < n; q += G) {
-        const int c = f.col(s + q);
-        double b[LM];
+    for (int q0 = gl; q0 < n; q0 += U * G) {
+        int c[U];
+        double b[U][LM];
 #pragma unroll
-        for (int i = 0; i < LM; ++i) b[i] = f.val(s + o[i] + q);
+        for (int u = 0; u < U; ++u) {
+            const int q = q0 + u * G < n ? q0 + u * G : q0;  // clamped: a cache hit, not accumulated
+            c[u] = f.col(s + q);
 #pragma unroll
-        for (int i = 1; i < LM; ++i) pin(b[i]);
-        double v[RM];
-#pragma unroll
-        for (int r = 0; r < RM; ++r) {
-            v[r] = a[r][0] * b[0];
-#pragma unroll
-            for (int i = 1; i < LM; ++i) v[r] += i < L ? a[r][i] * b[i] : 0.0;
+            for (int i = 0; i < LM; ++i) b[u][i] = f.val(s + o[i] + q);
         }
-        f.add_rows(c, v, R, stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 0; i < LM; ++i) pin(b[u][i]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (q0 + u * G >= n) break;
+            double v[RM];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) {
+                v[r] = a[r][0] * b[u][0];
+#pragma unroll
+                for (int i = 1; i < LM; ++i) {
+                    if constexpr (FULL)  // every visit of the sweep is a whole run: no masks
+                        v[r] = fma(a[r][i], b[u][i], v[r]);
+                    else
+                        v[r] += i < L ? a[r][i] * b[u][i] : 0.0;
+                }
+            }
+            f.add_rows(c[u], v, R, stride);
+        }
     }
 }
 
@@ -764,14 +786,17 @@ __device__ __forceinline__ void for_products_group(int a0, int a1, const int* __
                 double a[RM][1];
 #pragma unroll
                 for (int r = 0; r < RM; ++r) a[r][0] = __shfl(avr[r], h);
-                run_segment_group<1, RM>(f, sb, n, gl, G, a, 1, R, stride);
+                run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
             } else {
                 double a[RM][3];
 #pragma unroll
                 for (int r = 0; r < RM; ++r)
 #pragma unroll
                     for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h + i, 63));
-                run_segment_group<3, RM>(f, sb, n, gl, G, a, L, R, stride);
+                if (__ballot(n > 0 && L != 3) == 0)
+                    run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
+                else
+                    run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
             }
         }
     }
@@ -1204,7 +1229,7 @@ template <int NB>
 __device__ void append_block_rows(const unsigned char* binof, long long M, int* __restrict__ cnt,
                                   int* __restrict__ list) {
     constexpr int PER = SCAN_ITEMS / 1024;
-    static_assert(PER * 16 == 64 && NB <= 16, "one wave scans one bin's (pass, wave) counts");
+    static_assert(PER * 16 <= 64 && NB <= 16, "one wave scans one bin's (pass, wave) counts");
     __shared__ int wc[NB][PER * 16];  // [bin][pass*16 + wave]: members, then exclusive prefix
     __shared__ int nbase[NB];
     const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -1221,9 +1246,9 @@ __device__ void append_block_rows(const unsigned char* binof, long long M, int* 
     }
     __syncthreads();
     if (w >= 1 && w < NB) {  // wave x: exclusive prefix over (pass, wave); reserve the block's places
-        const int c = wc[w][lane];
+        const int c = lane < PER * 16 ? wc[w][lane] : 0;
         const int inc = wave_incl_scan(c);
-        wc[w][lane] = inc - c;
+        if (lane < PER * 16) wc[w][lane] = inc - c;
         if (lane == 63) nbase[w] = inc ? atomicAdd(&cnt[w], inc) : 0;
     }
     __syncthreads();

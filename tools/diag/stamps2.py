@@ -1,0 +1,27 @@
+"""Per-phase cycle totals of numeric rows (diag build 9), heads only, plus occupancy math."""
+import sys, ctypes, os
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[2]
+sys.path[:0] = [str(ROOT), str(ROOT / "mh-spgemm_amd")]
+os.environ["MHS_LIB"] = str(ROOT / "tools/diag/v9/libmhspgemm.so")
+import numpy as np, torch
+from mhspgemm import _lib
+import mhspgemm
+from mhspgemm import synth
+A = synth.SYNTH[sys.argv[1] if len(sys.argv) > 1 else "cant"](); A.H2D(0)
+tool = mhspgemm.Tool(0)
+L = _lib.lib(); L.mhs_diag_setup.argtypes = [ctypes.c_int, ctypes.c_void_p]
+dev = ctypes.c_void_p()
+assert L.mhs_diag_setup(A.M, ctypes.byref(dev)) == 0
+for i in range(3):
+    C, t = mhspgemm.spgemm(tool, A, A); C.release()
+buf = np.zeros(A.M * 8, np.uint64)
+L.mhs_memcpy(tool.ctx, buf.ctypes.data, dev, buf.nbytes, 1)
+ph = buf.reshape(A.M, 8).astype(np.float64)
+heads = ph[:, :6].sum(1) > 0
+names = ["prologue", "tiles(load/build)", "bases(+rmap)", "clear_acc", "accumulate", "output"]
+print("heads", heads.sum(), "of", A.M)
+for k, nm in enumerate(names):
+    print(f"{nm:20s} {ph[heads, k].mean():10.0f} cycles/head")
+tot = ph[heads, :6].sum()
+print("sum cycles over heads %.3e ; numeric ms %.4f" % (tot, t.Numeric))
