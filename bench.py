@@ -243,7 +243,7 @@ def main():
         ph["t_ref_getTotal"] = round(float(np.mean([p.getTotal() for p in phases])), 4)
         ph["note"] = "5 synchronised calls with per-phase events, after the timed region"
         out["phases_ms"] = ph
-        out["bins"] = {"symbolic": phases[-1].sym_bins[:5], "numeric": phases[-1].num_bins[:8]}
+        out["bins"] = {"symbolic": phases[-1].sym_bins[:6], "numeric": phases[-1].num_bins[:9]}
         if not args.no_cpu:
             med, threads, reps, one = cpu_baseline(A)
             out["cpu_baseline"] = {

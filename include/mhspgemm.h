@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 2
+#define MHS_ABI_VERSION 3
 
 typedef enum mhs_status {
     MHS_OK = 0,
@@ -67,8 +67,8 @@ typedef struct mhs_timing {
     double total_e2e;          /* everything, device-resident A,B -> device-resident C */
     uint64_t flop;             /* sum over A's nonzeros of nnz(B row)   (src/main.cu:102-107) */
     int64_t nnzC;
-    int32_t sym_bins[8];       /* rows per symbolic bin (0: empty rows) */
-    int32_t num_bins[8];       /* rows per numeric bin  (0: empty rows) */
+    int32_t sym_bins[16];      /* rows per symbolic bin (0: rows not processed: empty, or in a row group) */
+    int32_t num_bins[16];      /* rows per numeric bin  (0: likewise)                                  */
 } mhs_timing;
 
 typedef struct mhs_ctx mhs_ctx;

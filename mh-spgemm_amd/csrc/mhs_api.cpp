@@ -375,7 +375,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     launch_analyze(a, w, MB, s, out.ptr);
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[2], s));
     // ---- Calculate_C_nnz ------------------------------------------------------------
-    MHS_HIP(launch_symbolic(a, w, M, N, out.ptr, s, sym_grid, ctx->use_side ? ctx->side : nullptr, ctx->fork,
+    MHS_HIP(launch_symbolic(a, b, w, M, N, out.ptr, s, sym_grid, ctx->use_side ? ctx->side : nullptr, ctx->fork,
                             ctx->join));
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
@@ -384,7 +384,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         // the numeric bin offsets kernel publishes Stats to pinned host memory; the
         // host spins on the sequence number (no stream sync, no interrupt wake-up)
         const int seq = ++ctx->seq;
-        launch_scan_classify(M, w, out.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
+        launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
         MHS_HIP(hipGetLastError());
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
         rc = wait_published(ctx, s, seq);
@@ -467,7 +467,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         tm.total_ref = tm.total_e2e - tm.Form_mask_matrix_B;
         tm.flop = h.flop;
         tm.nnzC = h.nnzC;
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < 16; ++i) {
             tm.sym_bins[i] = i < NBINS ? h.sym_count[i] : 0;
             tm.num_bins[i] = i < NBINS ? h.num_count[i] : 0;
         }

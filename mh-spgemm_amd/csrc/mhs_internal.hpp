@@ -24,18 +24,23 @@ namespace mhs {
 
 constexpr int TILE_SHIFT = 6;  // 64-column tiles, one uint64 mask each (wave64 ballot width)
 constexpr int TILE_BITS = 64;
-constexpr int NBINS = 8;
+constexpr int NBINS = 16;  // capacity of the per-bin counters
 constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
 constexpr int SCAN_ITEMS = 1024;// rows per block in the row_ptr scan and the bin-list passes
 
 // Symbolic bins (by LDS need and tile work).
-enum SymBin : int { SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_NB = 5 };
+enum SymBin : int {
+    SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_TINY = 5, SYM_NB = 6
+};
+// Tiny rows (at most TINY_W products and A entries): a team of TINY_W lanes per row,
+// one product per lane, sorted by column in registers -- no table, no LDS.
+constexpr int TINY_W = 32;
 // Numeric bins (by LDS need and product work).
 // NUM_WSG / NUM_W16G: row groups (up to RG_MAX consecutive rows of A with one
 // column pattern, processed together by one wave: every B value loaded feeds R rows).
 enum NumBin : int {
     NUM_NONE = 0, NUM_WS = 1, NUM_W16 = 2, NUM_B256 = 3, NUM_B1024 = 4, NUM_GLOBAL = 5, NUM_WSG = 6,
-    NUM_W16G = 7, NUM_NB = 8
+    NUM_W16G = 7, NUM_TINY = 8, NUM_NB = 9
 };
 // Row groups: rows i-1, i of A with the same column pattern (FEM dofs of one node)
 // have C rows with one pattern.  Maximal runs are broken every RG_BREAK rows and cut
@@ -79,8 +84,6 @@ struct Stats {
     int num_count[NBINS];
     int num_global_need;           // max LDS-equivalent bytes of a global numeric row
     int final_done;                // k_scan_final blocks finished (last one publishes)
-    long long sym_start[NBINS];
-    long long num_start[NBINS];
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
 // kernel writes it and then `seq`, the host spins on `seq` instead of a stream sync.
@@ -213,9 +216,10 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);
 void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr);
 int analyze_blocks(long long nnzA, int M);
 
-hipError_t launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid,
-                           hipStream_t side = nullptr, hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
-void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max,
+hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s,
+                           int global_grid, hipStream_t side = nullptr, hipEvent_t fork = nullptr,
+                           hipEvent_t join = nullptr);
+void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
                           Published* pub, int seq);
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
                     int* Ccol, double* Cval, hipStream_t s, int global_grid, int dense_span_max);

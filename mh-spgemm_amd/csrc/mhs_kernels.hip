@@ -527,7 +527,8 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
         rtflop[row] = tf;
         rlo[row] = lo;
         rhi[row] = hi;
-        const int bin = sym_bin_of(f, tf, span);
+        const int nA = Aptr[row + 1] - Aptr[row];
+        const int bin = (f > 0 && f <= TINY_W && nA <= TINY_W) ? SYM_TINY : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
         if (bin == SYM_NONE) {
             Cptr[row] = 0;
@@ -1337,8 +1338,9 @@ __device__ void scan_partials(int nb, long long* __restrict__ part, Stats* __res
 }
 
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
-                                          int dense_span_max) {
+                                          int dense_span_max, int nA) {
     if (n == 0) return NUM_NONE;
+    if (flop <= TINY_W && nA <= TINY_W) return NUM_TINY;
     const long long need = num_need(span, t, n, dense_span_max);
     if (need <= NUM_WS_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WS;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16;
@@ -1349,8 +1351,9 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
 }
 
 // Grouped numeric bin of a group of R rows (NUM_NONE: run its rows one by one).
-__device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t, int R, int dense_span_max) {
-    if (R < 2 || n == 0) return NUM_NONE;
+__device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t, int R, int dense_span_max,
+                                                int nA) {
+    if (R < 2 || n == 0 || (flop <= TINY_W && nA <= TINY_W)) return NUM_NONE;  // tiny rows: one by one
     const long long need = num_need_rows(span, t, n, dense_span_max, R);
     if (need <= NUM_WSG_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WSG;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16G;
@@ -1387,6 +1390,7 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
                                                      const int* __restrict__ rhi,
                                                      const int* __restrict__ ctiles,
                                                      const unsigned char* __restrict__ grp,
+                                                     const int* __restrict__ Aptr,
                                                      int* __restrict__ list, Stats* __restrict__ stats,
                                                      int dense_span_max, Published* pub, int seq) {
     constexpr int PER = SCAN_ITEMS / 1024;
@@ -1421,11 +1425,12 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
             // a group runs as one item when its R accumulators fit a wave bin; its
             // members decide alike (same pattern, same sizes) and then stay out
             const int gh = (g & GRP_CONT) ? grp[i - (g & 0x7F)] : g;
-            const int gb = num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max);
+            const int nA = Aptr[i + 1] - Aptr[i];
+            const int gb = num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max, nA);
             if (gb != NUM_NONE)
                 nbin = (g & GRP_CONT) ? NUM_NONE : gb;
             else
-                nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max);
+                nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max, nA);
         }
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
         off += v[k];
@@ -1668,6 +1673,127 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
                                                      reg, counter, stage);
 }
 
+// ------------------------------------------------------------- tiny rows ---
+// Rows of at most W products (and W A entries): a team of W lanes per row, one
+// product per lane.  Lane p finds its A entry by a binary search over the team's
+// inclusive scan of B-row lengths, loads its (column, value), and the team sorts the
+// pairs by column (bitonic, in registers); equal columns are adjacent: heads count
+// the row (symbolic) or close a segmented sum (numeric).  No table, no LDS, and every
+// lane busy -- where a wave per row would idle 63 lanes through ten dependent loads.
+struct TinyArgs {
+    int M, count;  // count: numeric only (symbolic reads its bin size on the device)
+    const int* Aptr;
+    const int* Acol;
+    const double* Aval;
+    const int4* bmeta;
+    const int* Bcol;
+    const double* Bval;
+    const int* list;  // the tiny bin's rows
+    const Stats* stats;
+    const unsigned char* grp;
+    int* Cptr;
+    int* ctiles;
+    int* Ccol;
+    double* Cval;
+};
+
+template <int W, bool NUMERIC>
+__global__ __launch_bounds__(256) void k_tiny(TinyArgs a) {
+    const int lane = lane_id();
+    const int tl = lane & (W - 1);   // lane in the team
+    const int tb = lane & ~(W - 1);  // the team's first lane
+    const unsigned long long tmask = W == 64 ? ~0ull : (((1ull << (W & 63)) - 1) << tb);
+    const unsigned long long below = tmask & lanemask_lt();
+    const int count = NUMERIC ? a.count : a.stats->sym_count[SYM_TINY];
+    const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W));
+    // the wave iterates while any of its teams has a row (shuffles need every lane)
+    for (int it = rw.first; __ballot(it < rw.end) != 0; it += rw.stride) {
+        const bool live = it < rw.end;
+        const int row = live ? a.list[it] : 0;
+        const int a0 = live ? a.Aptr[row] : 0, nA = live ? a.Aptr[row + 1] - a0 : 0;
+        int st = 0, len = 0;
+        double av = 0.0;
+        if (tl < nA) {
+            const int4 m = a.bmeta[a.Acol[a0 + tl]];
+            st = m.x;
+            len = m.y;
+            if (NUMERIC) av = a.Aval[a0 + tl];
+        }
+        int incl = len;  // inclusive scan of the B-row lengths over the team
+#pragma unroll
+        for (int d = 1; d < W; d <<= 1) {
+            const int o = __shfl_up(incl, d, W);
+            if (tl >= d) incl += o;
+        }
+        const int flop = __shfl(incl, tb + W - 1);
+        int j = 0;  // this lane's product belongs to entry j: the first with incl_j > tl
+#pragma unroll
+        for (int step = W / 2; step >= 1; step >>= 1) {
+            const int v = __shfl(incl, tb + j + step - 1);
+            if (v <= tl) j += step;
+        }
+        const bool valid = tl < flop;
+        const int src = tb + (valid ? j : 0);
+        const int stj = __shfl(st, src);
+        const int exj = __shfl(incl - len, src);
+        const double avj = NUMERIC ? __shfl(av, src) : 0.0;  // shuffles outside the branch: every lane
+        int c = INT_MAX;
+        double v = 0.0;
+        if (valid) {
+            const int q = stj + (tl - exj);
+            c = a.Bcol[q];
+            if (NUMERIC) v = avj * a.Bval[q];
+        }
+        // bitonic sort of (c, v) by c, ascending, within the team
+#pragma unroll
+        for (int k = 2; k <= W; k <<= 1) {
+#pragma unroll
+            for (int d = k >> 1; d > 0; d >>= 1) {
+                const int oc = __shfl_xor(c, d, W);
+                double ov = 0.0;
+                if (NUMERIC) ov = __shfl_xor(v, d, W);
+                const bool asc = (tl & k) == 0, low = (tl & d) == 0;
+                if (low == asc ? oc < c : oc > c) {
+                    c = oc;
+                    v = ov;
+                }
+            }
+        }
+        const int pc = __shfl_up(c, 1, W);
+        const bool head = c != INT_MAX && (tl == 0 || pc != c);
+        const unsigned long long hb = __ballot(head) & tmask;
+        if constexpr (!NUMERIC) {
+            const bool thead = head && (tl == 0 || (pc >> TILE_SHIFT) != (c >> TILE_SHIFT));
+            const int nt = __popcll(__ballot(thead) & tmask);
+            const int R = live ? (int)a.grp[row] : 0;  // a group head: its rows share the count
+            if (tl < R) {
+                a.Cptr[row + tl] = __popcll(hb);
+                a.ctiles[row + tl] = nt;
+            }
+        } else {
+            // segmented inclusive sum, segments start at heads
+            double sum = v;
+            bool seen = head;
+#pragma unroll
+            for (int d = 1; d < W; d <<= 1) {
+                const double os = __shfl_up(sum, d, W);
+                const int of = __shfl_up((int)seen, d, W);
+                if (tl >= d && !seen) {
+                    sum += os;
+                    seen = of != 0;
+                }
+            }
+            const int nc = __shfl_down(c, 1, W);
+            const bool last = c != INT_MAX && (tl == W - 1 || nc != c);
+            if (live && last) {
+                const int pos = a.Cptr[row] + __popcll(hb & (below | (1ull << lane))) - 1;
+                a.Ccol[pos] = c;
+                a.Cval[pos] = sum;
+            }
+        }
+    }
+}
+
 // -------------------------------------------------------------- launchers ---
 
 static int pick_group(long long nnz, int rows, int gmax = 64) {
@@ -1755,8 +1881,8 @@ size_t sym_global_bytes_per_block(int N) {
     return (size_t)hash_slots(span_max) * 16;
 }
 
-hipError_t launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid,
-                           hipStream_t side, hipEvent_t fork, hipEvent_t join) {
+hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s,
+                           int global_grid, hipStream_t side, hipEvent_t fork, hipEvent_t join) {
     if (M <= 0) return hipSuccess;
     SymArgs a;
     a.M = M;
@@ -1796,6 +1922,21 @@ hipError_t launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr,
     a.bin = SYM_WAVE;
     hipLaunchKernelGGL(k_sym_wave<SYM_WAVE_BYTES>, dim3(round8((M + WPB - 1) / WPB, 2048)), dim3(256),
                        WPB * SYM_WAVE_BYTES, s, a);
+    {
+        TinyArgs t{};
+        t.M = M;
+        t.Aptr = A.ptr;
+        t.Acol = A.col;
+        t.bmeta = w.bmeta;
+        t.Bcol = B.col;
+        t.list = w.bin_list + (long long)(SYM_TINY - 1) * M;
+        t.stats = w.stats;
+        t.grp = w.grp;
+        t.Cptr = Cptr;
+        t.ctiles = w.ctiles;
+        hipLaunchKernelGGL((k_tiny<TINY_W, false>), dim3(round8((M + 256 / TINY_W - 1) / (256 / TINY_W), 2048)),
+                           dim3(256), 0, s, t);
+    }
     if (side) {
         hipError_t e = hipEventRecord(join, side);
         if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
@@ -1804,13 +1945,13 @@ hipError_t launch_symbolic(const Csr& A, const Work& w, int M, int N, int* Cptr,
     return hipSuccess;
 }
 
-void launch_scan_classify(int M, const Work& w, int* Cptr, hipStream_t s, int dense_span_max, Published* pub,
-                          int seq) {
+void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
+                          Published* pub, int seq) {
     const int nb = (M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS;
     long long* part = (long long*)w.scan_part;
     hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.stats, w.blkflop, w.nflop);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.rflop, w.rlo, w.rhi,
-                       w.ctiles, w.grp, w.bin_list, w.stats, dense_span_max, pub, seq);
+                       w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq);
 }
 
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
@@ -1861,6 +2002,24 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
         a.list = w.bin_list + (long long)(NUM_W16 - 1) * A.M;
         hipLaunchKernelGGL(k_num_wave<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
                            WPB * NUM_W16_BYTES, s, a);
+    }
+    if (h.num_count[NUM_TINY] > 0) {
+        TinyArgs t{};
+        t.M = A.M;
+        t.count = h.num_count[NUM_TINY];
+        t.Aptr = A.ptr;
+        t.Acol = A.col;
+        t.Aval = A.val;
+        t.bmeta = w.bmeta;
+        t.Bcol = B.col;
+        t.Bval = B.val;
+        t.list = w.bin_list + (long long)(NUM_TINY - 1) * A.M;
+        t.Cptr = Cptr;
+        t.Ccol = Ccol;
+        t.Cval = Cval;
+        const int teams = 256 / TINY_W;
+        hipLaunchKernelGGL((k_tiny<TINY_W, true>), dim3(round8((t.count + teams - 1) / teams, 4096)), dim3(256), 0,
+                           s, t);
     }
     if (h.num_count[NUM_W16G] > 0) {
         const int count = a.count = h.num_count[NUM_W16G];

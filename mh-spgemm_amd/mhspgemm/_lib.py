@@ -40,7 +40,7 @@ class mhs_timing(ctypes.Structure):
                 ("numeric_binning", ctypes.c_double), ("Malloc_C_col_val", ctypes.c_double),
                 ("Numeric", ctypes.c_double), ("total_ref", ctypes.c_double),
                 ("total_e2e", ctypes.c_double), ("flop", ctypes.c_uint64), ("nnzC", ctypes.c_int64),
-                ("sym_bins", ctypes.c_int32 * 8), ("num_bins", ctypes.c_int32 * 8)]
+                ("sym_bins", ctypes.c_int32 * 16), ("num_bins", ctypes.c_int32 * 16)]
 
 
 class mhs_host_csr(ctypes.Structure):

@@ -102,8 +102,8 @@ class Timing:
     total_e2e: float = 0.0
     flop: int = 0
     nnzC: int = 0
-    sym_bins: list = field(default_factory=lambda: [0] * 8)
-    num_bins: list = field(default_factory=lambda: [0] * 8)
+    sym_bins: list = field(default_factory=lambda: [0] * 16)
+    num_bins: list = field(default_factory=lambda: [0] * 16)
 
     PHASES = ("mem_alloc", "Form_mask_matrix_B", "Calculate_C_nnz", "Malloc_C_col_val",
               "Numeric", "symbolic_binning", "numeric_binning", "total_e2e")

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.lib_path()], capture_output=True, text=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert set(names) <= exported
-    assert L.mhs_abi_version() == 2
+    assert L.mhs_abi_version() == 3
 
 
 def test_library_is_gfx950_code_object():

@@ -1,10 +1,2 @@
-export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trw -o run -- python3 tools/diag/run_phases.py mh-spgemm_amd/mhspgemm webbase-1M > gpurun_out/trw.log 2>&1
-timeout -k 10 300 python3 -c "
-import sys; sys.path[:0]=['.','mh-spgemm_amd']
-import torch, mhspgemm
-from mhspgemm import synth
-A = synth.SYNTH['webbase-1M'](); A.H2D(0)
-t = mhspgemm.Tool(0)
-C, tm = mhspgemm.spgemm(t, A, A)
-print('sym', list(tm.sym_bins), 'num', list(tm.num_bins), 'nnzC', tm.nnzC)
-" > gpurun_out/wbins.log 2>&1
+timeout -k 10 400 python -m pytest tests -q -m gpu -x > gpurun_out/t_tiny.log 2>&1; tail -1 gpurun_out/t_tiny.log
+for m in cant cop20k_A webbase-1M scircuit mac_econ_fwd500; do MATRIX=$m RUNPY=tools/diag/run_phases.py tools/diag/ab.sh "new||mh-spgemm_amd/mhspgemm" | sed "s/^/$m /" >> gpurun_out/ab_tiny.log 2>&1 || exit $?; done
