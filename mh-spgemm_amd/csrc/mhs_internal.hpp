@@ -29,18 +29,31 @@ constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
 constexpr int SCAN_ITEMS = 1024;// rows per block in the row_ptr scan and the bin-list passes
 
 // Symbolic bins (by LDS need and tile work).
+// Tiny rows: a team of W lanes per row holding K products per lane (flop <= W*K,
+// nA <= W), sorted by column in registers -- no table, no LDS.  Classes, smallest
+// first; a row takes the first class it fits.
+constexpr int TINY_NC = 4;
+constexpr int TINY_EBITS = 7;              // numeric sort key = (column << 7) | element (W*K <= 128)
+constexpr int TINY_NUM_NMAX = 1 << 24;     // ... so the numeric tiny classes need N <= 2^24 columns
+__host__ __device__ constexpr int tiny_w(int c) { return c == 0 ? 8 : 32; }
+__host__ __device__ constexpr int tiny_k(int c) { return c <= 1 ? 1 : (c == 2 ? 2 : 4); }
+__host__ __device__ inline int tiny_class(int flop, int nA) {
+    if (flop <= 0) return -1;
+    for (int c = 0; c < TINY_NC; ++c)
+        if (flop <= tiny_w(c) * tiny_k(c) && nA <= tiny_w(c)) return c;
+    return -1;
+}
 enum SymBin : int {
-    SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_TINY = 5, SYM_NB = 6
+    SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_TINY = 5,
+    SYM_WM = SYM_TINY + TINY_NC,  // wave per row with a 10 KiB table (scattered rows of a few hundred tiles)
+    SYM_NB
 };
-// Tiny rows (at most TINY_W products and A entries): a team of TINY_W lanes per row,
-// one product per lane, sorted by column in registers -- no table, no LDS.
-constexpr int TINY_W = 32;
 // Numeric bins (by LDS need and product work).
 // NUM_WSG / NUM_W16G: row groups (up to RG_MAX consecutive rows of A with one
 // column pattern, processed together by one wave: every B value loaded feeds R rows).
 enum NumBin : int {
     NUM_NONE = 0, NUM_WS = 1, NUM_W16 = 2, NUM_B256 = 3, NUM_B1024 = 4, NUM_GLOBAL = 5, NUM_WSG = 6,
-    NUM_W16G = 7, NUM_TINY = 8, NUM_NB = 9
+    NUM_W16G = 7, NUM_TINY = 8, NUM_NB = NUM_TINY + TINY_NC
 };
 // Row groups: rows i-1, i of A with the same column pattern (FEM dofs of one node)
 // have C rows with one pattern.  Maximal runs are broken every RG_BREAK rows and cut
@@ -50,8 +63,9 @@ constexpr int RG_BREAK = 96;  // a multiple of 2, 3, 4 and 6: dof blocks of thos
 constexpr int GRP_CONT = 0x80;
 
 // Per-team LDS budgets (bytes).  The wave kernels carve one region per wave.
-constexpr int SYM_WAVE_BYTES = 4096;
+constexpr int SYM_WAVE_BYTES = 5120;   // 4 waves x 5 KiB: 8 blocks (32 waves, the CU's cap) per CU
 constexpr int SYM_WAVE_WORK = 4096;     // tile products a single wave takes on
+constexpr int SYM_WM_BYTES = 10240;   // 4 waves x 10 KiB: 4 blocks (16 waves) per CU
 constexpr int SYM_B256_BYTES = 32768;
 constexpr int SYM_B256_WORK = 1 << 20;
 constexpr int NUM_WS_BYTES = 5120;   // 4 waves x 5 KiB = 20 KiB/block: 8 blocks (32 waves) per CU
@@ -108,17 +122,23 @@ __host__ __device__ inline int ilog2(int x) {  // x power of two
     while ((1 << l) < x) ++l;
     return l;
 }
-// Open-addressed table size for up to `bound` distinct keys: load <= 1/2.
+// Open-addressed table size for up to `bound` distinct keys: load <= 2/3 (linear
+// probing stays short; a tighter table lets more rows share a CU's LDS, and the
+// small-row phases are bound by rows in flight, not by probes).
 __host__ __device__ inline int hash_slots(int bound) {
-    int h = next_pow2(2 * (bound < 1 ? 1 : bound));
+    const int b = bound < 1 ? 1 : bound;
+    const int h = next_pow2(b + (b >> 1) + 1);
     return h < 16 ? 16 : h;
 }
 __host__ __device__ inline long long align16(long long x) { return (x + 15) & ~15LL; }
 
-// Symbolic tile table: direct-mapped over the row's tile span, or hashed.
+// Symbolic tile table: direct-mapped over the row's tile span (no keys, no CAS) when
+// the span is not much wider than the table a hash would need and the direct table
+// does not push the row into a bigger bin than the hash would; else hashed.
 __host__ __device__ inline bool sym_direct(int span, int tflop) {
-    int bound = tflop < span ? tflop : span;
-    return span <= hash_slots(bound);
+    const int bound = tflop < span ? tflop : span;
+    const int h = hash_slots(bound);
+    return span <= 2 * h && (span <= h || (long long)span * 16 <= 4096);
 }
 __host__ __device__ inline long long sym_need(int span, int tflop) {
     int bound = tflop < span ? tflop : span;
@@ -202,6 +222,7 @@ struct Work {
     unsigned char* asame;    // M: row has the column pattern of row-1 (k_analyze)
     unsigned char* grp;      // M: row groups (k_bin_list; see RG_MAX)
     int groups;              // form row groups (0: every row alone)
+    int tiny_num;            // numeric tiny classes allowed (B.N <= TINY_NUM_NMAX)
     int* bin_list;           // (NUM_NB-1) * M: bin x's rows at (x-1)*M (symbolic bins, then numeric bins)
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count

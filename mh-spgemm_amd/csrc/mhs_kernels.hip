@@ -247,16 +247,19 @@ __device__ __forceinline__ StagedChunk stage_chunk(int lane, int jb, int a1,
 // stride through it.  Speed only -- any placement gives the same result.
 struct RowWalk {
     int first, end, stride;
-    __device__ RowWalk(int count, int teams_per_block, int team) {
-        if ((gridDim.x & 7) == 0) {
-            const int g = blockIdx.x & 7, nbg = gridDim.x >> 3, bi = blockIdx.x >> 3;
+    __device__ RowWalk(int count, int teams_per_block, int team)
+        : RowWalk(count, teams_per_block, team, (int)blockIdx.x, (int)gridDim.x) {}
+    // blocks [0, nb) of a sub-grid (bid = index in it)
+    __device__ RowWalk(int count, int teams_per_block, int team, int bid, int nb) {
+        if ((nb & 7) == 0) {
+            const int g = bid & 7, nbg = nb >> 3, bi = bid >> 3;
             first = (int)((long long)count * g / 8) + bi * teams_per_block + team;
             end = (int)((long long)count * (g + 1) / 8);
             stride = nbg * teams_per_block;
         } else {
-            first = blockIdx.x * teams_per_block + team;
+            first = bid * teams_per_block + team;
             end = count;
-            stride = gridDim.x * teams_per_block;
+            stride = nb * teams_per_block;
         }
     }
 };
@@ -449,6 +452,7 @@ __device__ __forceinline__ int sym_bin_of(int flop, int tflop, int span) {
     if (flop == 0) return SYM_NONE;
     const long long need = sym_need(span, tflop);
     if (need <= SYM_WAVE_BYTES - WAVE_HDR && tflop <= SYM_WAVE_WORK) return SYM_WAVE;
+    if (need <= SYM_WM_BYTES - WAVE_HDR && tflop <= SYM_WAVE_WORK) return SYM_WM;
     if (need <= SYM_B256_BYTES - BLOCK_HDR && tflop <= SYM_B256_WORK) return SYM_B256;
     if (need <= B1024_BYTES) return SYM_B1024;
     return SYM_GLOBAL;
@@ -528,7 +532,8 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
         rlo[row] = lo;
         rhi[row] = hi;
         const int nA = Aptr[row + 1] - Aptr[row];
-        const int bin = (f > 0 && f <= TINY_W && nA <= TINY_W) ? SYM_TINY : sym_bin_of(f, tf, span);
+        const int tc = tiny_class(f, nA);
+        const int bin = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
         if (bin == SYM_NONE) {
             Cptr[row] = 0;
@@ -1338,9 +1343,10 @@ __device__ void scan_partials(int nb, long long* __restrict__ part, Stats* __res
 }
 
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
-                                          int dense_span_max, int nA) {
+                                          int dense_span_max, int nA, bool tiny_ok) {
     if (n == 0) return NUM_NONE;
-    if (flop <= TINY_W && nA <= TINY_W) return NUM_TINY;
+    const int tc = tiny_ok ? tiny_class(flop, nA) : -1;
+    if (tc >= 0) return NUM_TINY + tc;
     const long long need = num_need(span, t, n, dense_span_max);
     if (need <= NUM_WS_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WS;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16;
@@ -1352,8 +1358,8 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
 
 // Grouped numeric bin of a group of R rows (NUM_NONE: run its rows one by one).
 __device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t, int R, int dense_span_max,
-                                                int nA) {
-    if (R < 2 || n == 0 || (flop <= TINY_W && nA <= TINY_W)) return NUM_NONE;  // tiny rows: one by one
+                                                int nA, bool tiny_ok) {
+    if (R < 2 || n == 0 || (tiny_ok && tiny_class(flop, nA) >= 0)) return NUM_NONE;  // tiny rows: one by one
     const long long need = num_need_rows(span, t, n, dense_span_max, R);
     if (need <= NUM_WSG_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WSG;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16G;
@@ -1392,7 +1398,7 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
                                                      const unsigned char* __restrict__ grp,
                                                      const int* __restrict__ Aptr,
                                                      int* __restrict__ list, Stats* __restrict__ stats,
-                                                     int dense_span_max, Published* pub, int seq) {
+                                                     int dense_span_max, Published* pub, int seq, int tiny_ok) {
     constexpr int PER = SCAN_ITEMS / 1024;
     __shared__ long long ws[16];
     const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -1426,11 +1432,12 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
             // members decide alike (same pattern, same sizes) and then stay out
             const int gh = (g & GRP_CONT) ? grp[i - (g & 0x7F)] : g;
             const int nA = Aptr[i + 1] - Aptr[i];
-            const int gb = num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max, nA);
+            const int gb = num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max, nA, tiny_ok);
             if (gb != NUM_NONE)
                 nbin = (g & GRP_CONT) ? NUM_NONE : gb;
             else
-                nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max, nA);
+                nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max, nA,
+                                  tiny_ok);
         }
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
         off += v[k];
@@ -1674,21 +1681,24 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
 }
 
 // ------------------------------------------------------------- tiny rows ---
-// Rows of at most W products (and W A entries): a team of W lanes per row, one
-// product per lane.  Lane p finds its A entry by a binary search over the team's
-// inclusive scan of B-row lengths, loads its (column, value), and the team sorts the
-// pairs by column (bitonic, in registers); equal columns are adjacent: heads count
-// the row (symbolic) or close a segmented sum (numeric).  No table, no LDS, and every
-// lane busy -- where a wave per row would idle 63 lanes through ten dependent loads.
+// Rows of at most W*K products (and W A entries): a team of W lanes per row holding
+// K products per lane, slot-major (product p = i*W + lane in slot i).  Lane p finds
+// its A entry by a binary search over the team's inclusive scan of B-row lengths,
+// loads its (column, value), and the team sorts the W*K pairs by column (bitonic in
+// registers: element e = i*W + lane, partners across lanes by shuffles for d < W and
+// across slots in the lane for d >= W); equal columns are then adjacent: heads count
+// the row (symbolic) or close a segmented sum (numeric).  No table and no LDS, and
+// several rows per wave -- where a wave per row would idle most lanes through ten
+// dependent loads.
 struct TinyArgs {
-    int M, count;  // count: numeric only (symbolic reads its bin size on the device)
+    int M, count, bin;  // count: numeric only (symbolic reads its bin's size on the device)
     const int* Aptr;
     const int* Acol;
     const double* Aval;
     const int4* bmeta;
     const int* Bcol;
     const double* Bval;
-    const int* list;  // the tiny bin's rows
+    const int* list;  // the bin's rows
     const Stats* stats;
     const unsigned char* grp;
     int* Cptr;
@@ -1697,20 +1707,23 @@ struct TinyArgs {
     double* Cval;
 };
 
-template <int W, bool NUMERIC>
-__global__ __launch_bounds__(256) void k_tiny(TinyArgs a) {
+template <int W, int K, bool NUMERIC>
+__device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
+    static_assert((W & (W - 1)) == 0 && W <= 64 && (K & (K - 1)) == 0 && W * K <= (1 << TINY_EBITS), "team shape");
+    constexpr int LW = W == 8 ? 3 : W == 16 ? 4 : W == 32 ? 5 : 6;
     const int lane = lane_id();
     const int tl = lane & (W - 1);   // lane in the team
     const int tb = lane & ~(W - 1);  // the team's first lane
     const unsigned long long tmask = W == 64 ? ~0ull : (((1ull << (W & 63)) - 1) << tb);
     const unsigned long long below = tmask & lanemask_lt();
-    const int count = NUMERIC ? a.count : a.stats->sym_count[SYM_TINY];
-    const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W));
+    const int count = NUMERIC ? a.count : a.stats->sym_count[a.bin];
+    const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W), bid, nb);
     // the wave iterates while any of its teams has a row (shuffles need every lane)
     for (int it = rw.first; __ballot(it < rw.end) != 0; it += rw.stride) {
         const bool live = it < rw.end;
         const int row = live ? a.list[it] : 0;
         const int a0 = live ? a.Aptr[row] : 0, nA = live ? a.Aptr[row + 1] - a0 : 0;
+        const int c0 = (NUMERIC && live) ? a.Cptr[row] : 0;  // issued early: off the tail's chain
         int st = 0, len = 0;
         double av = 0.0;
         if (tl < nA) {
@@ -1723,74 +1736,163 @@ __global__ __launch_bounds__(256) void k_tiny(TinyArgs a) {
 #pragma unroll
         for (int d = 1; d < W; d <<= 1) {
             const int o = __shfl_up(incl, d, W);
-            if (tl >= d) incl += o;
+            incl += tl >= d ? o : 0;
         }
         const int flop = __shfl(incl, tb + W - 1);
-        int j = 0;  // this lane's product belongs to entry j: the first with incl_j > tl
+        const int excl = incl - len;
+        // sort keys: symbolic the column; numeric (column << TINY_EBITS) | element, the
+        // value stays with its element and is fetched once after the sort
+        unsigned key[K];
+        double v[K];
 #pragma unroll
-        for (int step = W / 2; step >= 1; step >>= 1) {
-            const int v = __shfl(incl, tb + j + step - 1);
-            if (v <= tl) j += step;
-        }
-        const bool valid = tl < flop;
-        const int src = tb + (valid ? j : 0);
-        const int stj = __shfl(st, src);
-        const int exj = __shfl(incl - len, src);
-        const double avj = NUMERIC ? __shfl(av, src) : 0.0;  // shuffles outside the branch: every lane
-        int c = INT_MAX;
-        double v = 0.0;
-        if (valid) {
-            const int q = stj + (tl - exj);
-            c = a.Bcol[q];
-            if (NUMERIC) v = avj * a.Bval[q];
-        }
-        // bitonic sort of (c, v) by c, ascending, within the team
+        for (int i = 0; i < K; ++i) {
+            const int p = i * W + tl;
+            int j = 0;  // product p belongs to entry j: the first with incl_j > p
 #pragma unroll
-        for (int k = 2; k <= W; k <<= 1) {
+            for (int step = W / 2; step >= 1; step >>= 1) {
+                const int x = __shfl(incl, tb + j + step - 1);
+                j += x <= p ? step : 0;
+            }
+            const bool valid = p < flop;
+            const int src = tb + (valid ? j : 0);
+            const int stj = __shfl(st, src);
+            const int exj = __shfl(excl, src);
+            const double avj = NUMERIC ? __shfl(av, src) : 0.0;  // shuffles outside the branch: every lane
+            key[i] = 0xFFFFFFFFu;
+            v[i] = 0.0;
+            if (valid) {
+                const int q = stj + (p - exj);
+                const unsigned c = (unsigned)a.Bcol[q];
+                key[i] = NUMERIC ? (c << TINY_EBITS) | (unsigned)p : c;
+                if (NUMERIC) v[i] = avj * a.Bval[q];
+            }
+        }
+        // bitonic sort of the keys, ascending, over e = i*W + tl (compare-exchange by selects)
+#pragma unroll
+        for (int k = 2; k <= W * K; k <<= 1) {
 #pragma unroll
             for (int d = k >> 1; d > 0; d >>= 1) {
-                const int oc = __shfl_xor(c, d, W);
-                double ov = 0.0;
-                if (NUMERIC) ov = __shfl_xor(v, d, W);
-                const bool asc = (tl & k) == 0, low = (tl & d) == 0;
-                if (low == asc ? oc < c : oc > c) {
-                    c = oc;
-                    v = ov;
+                if (d < W) {
+                    unsigned ok[K];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) ok[i] = (unsigned)__shfl_xor((int)key[i], d, W);
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const bool asc = ((i * W + tl) & k) == 0, low = (tl & d) == 0;
+                        const bool take = (low == asc) ? ok[i] < key[i] : ok[i] > key[i];
+                        key[i] = take ? ok[i] : key[i];
+                    }
+                } else {
+                    const int ds = d / W;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        if (i & ds) continue;
+                        const int j = i | ds;
+                        const bool asc = ((i * W + tl) & k) == 0;
+                        const unsigned lo_ = key[i] < key[j] ? key[i] : key[j];
+                        const unsigned hi_ = key[i] < key[j] ? key[j] : key[i];
+                        key[i] = asc ? lo_ : hi_;
+                        key[j] = asc ? hi_ : lo_;
+                    }
                 }
             }
         }
-        const int pc = __shfl_up(c, 1, W);
-        const bool head = c != INT_MAX && (tl == 0 || pc != c);
-        const unsigned long long hb = __ballot(head) & tmask;
+        int c[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) c[i] = key[i] == 0xFFFFFFFFu ? INT_MAX : (int)(NUMERIC ? key[i] >> TINY_EBITS : key[i]);
+        if constexpr (NUMERIC) {  // each sorted slot fetches its element's value
+            double vs[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int e = (int)(key[i] & ((1u << TINY_EBITS) - 1));
+                const int srcl = tb + (e & (W - 1)), slot = e >> LW;
+                double x = 0.0;
+#pragma unroll
+                for (int s2 = 0; s2 < K; ++s2) {
+                    const double y = __shfl(v[s2], srcl);
+                    x = slot == s2 ? y : x;
+                }
+                vs[i] = c[i] == INT_MAX ? 0.0 : x;
+            }
+#pragma unroll
+            for (int i = 0; i < K; ++i) v[i] = vs[i];
+        }
+        // heads: element e differs from e-1 (slot i lane tl-1, or slot i-1 lane W-1)
+        bool head[K];
+        int nnz = 0, ntl = 0;
+        int prev_last = INT_MAX;  // slot i-1's last element (lane W-1)
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const int up = __shfl_up(c[i], 1, W);
+            const int pc = tl == 0 ? (i == 0 ? -1 : prev_last) : up;
+            head[i] = c[i] != INT_MAX && pc != c[i];
+            if constexpr (!NUMERIC) {
+                const bool thead = c[i] != INT_MAX && (pc < 0 || (pc >> TILE_SHIFT) != (c[i] >> TILE_SHIFT));
+                ntl += __popcll(__ballot(thead) & tmask);
+            }
+            nnz += __popcll(__ballot(head[i]) & tmask);
+            prev_last = __shfl(c[i], tb + W - 1);
+        }
         if constexpr (!NUMERIC) {
-            const bool thead = head && (tl == 0 || (pc >> TILE_SHIFT) != (c >> TILE_SHIFT));
-            const int nt = __popcll(__ballot(thead) & tmask);
             const int R = live ? (int)a.grp[row] : 0;  // a group head: its rows share the count
             if (tl < R) {
-                a.Cptr[row + tl] = __popcll(hb);
-                a.ctiles[row + tl] = nt;
+                a.Cptr[row + tl] = nnz;
+                a.ctiles[row + tl] = ntl;
             }
         } else {
-            // segmented inclusive sum, segments start at heads
-            double sum = v;
-            bool seen = head;
+            // segmented inclusive sums (segments start at heads), carried across slots
+            double carry = 0.0;  // open segment's sum at the end of slot i-1
+            int rank0 = 0;       // heads in slots < i
 #pragma unroll
-            for (int d = 1; d < W; d <<= 1) {
-                const double os = __shfl_up(sum, d, W);
-                const int of = __shfl_up((int)seen, d, W);
-                if (tl >= d && !seen) {
-                    sum += os;
-                    seen = of != 0;
+            for (int i = 0; i < K; ++i) {
+                double sum = v[i];
+                bool seen = head[i];
+#pragma unroll
+                for (int d = 1; d < W; d <<= 1) {
+                    const double os = __shfl_up(sum, d, W);
+                    const int of = __shfl_up((int)seen, d, W);
+                    const bool add = tl >= d && !seen;
+                    sum += add ? os : 0.0;
+                    seen = add ? of != 0 : seen;
                 }
-            }
-            const int nc = __shfl_down(c, 1, W);
-            const bool last = c != INT_MAX && (tl == W - 1 || nc != c);
-            if (live && last) {
-                const int pos = a.Cptr[row] + __popcll(hb & (below | (1ull << lane))) - 1;
-                a.Ccol[pos] = c;
-                a.Cval[pos] = sum;
+                sum += seen ? 0.0 : carry;  // the segment began in an earlier slot
+                const int nc = __shfl_down(c[i], 1, W);
+                const int nxt = i + 1 < K ? __shfl(c[i + 1 < K ? i + 1 : i], tb) : INT_MAX;
+                const int next = tl == W - 1 ? nxt : nc;
+                const bool last = c[i] != INT_MAX && next != c[i];
+                const unsigned long long hb = __ballot(head[i]) & tmask;
+                if (live && last) {
+                    const int pos = c0 + rank0 + __popcll(hb & (below | (1ull << lane))) - 1;
+                    a.Ccol[pos] = c[i];
+                    a.Cval[pos] = sum;
+                }
+                carry = __shfl(sum, tb + W - 1);
+                rank0 += __popcll(hb);
             }
         }
+    }
+}
+
+template <int W, int K>
+__global__ __launch_bounds__(256) void k_tiny_num(TinyArgs a) {
+    tiny_rows<W, K, true>(a, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// Every symbolic tiny class in one launch (the bins' sizes are on the device): blocks
+// [TINY_SYM_GRID*c, TINY_SYM_GRID*(c+1)) walk class c's list.
+constexpr int TINY_SYM_GRID = 1024;
+__global__ __launch_bounds__(256) void k_tiny_sym(TinyArgs a) {
+    const int c = (int)blockIdx.x / TINY_SYM_GRID, bid = (int)blockIdx.x % TINY_SYM_GRID;
+    static_assert(TINY_NC == 4 && tiny_w(0) == 8 && tiny_k(0) == 1 && tiny_w(1) == 32 && tiny_k(1) == 1 &&
+                      tiny_w(2) == 32 && tiny_k(2) == 2 && tiny_w(3) == 32 && tiny_k(3) == 4,
+                  "k_tiny_sym / launch_tiny instantiate the classes of tiny_class()");
+    a.bin = SYM_TINY + c;
+    a.list += (long long)c * a.M;
+    switch (c) {
+    case 0: tiny_rows<8, 1, false>(a, bid, TINY_SYM_GRID); break;
+    case 1: tiny_rows<32, 1, false>(a, bid, TINY_SYM_GRID); break;
+    case 2: tiny_rows<32, 2, false>(a, bid, TINY_SYM_GRID); break;
+    default: tiny_rows<32, 4, false>(a, bid, TINY_SYM_GRID); break;
     }
 }
 
@@ -1881,6 +1983,20 @@ size_t sym_global_bytes_per_block(int N) {
     return (size_t)hash_slots(span_max) * 16;
 }
 
+// Numeric tiny class c, `rows` rows.
+static void launch_tiny_num(int c, int rows, const TinyArgs& t, hipStream_t s) {
+#define MHS_TINY(WW, KK)                                                                                  \
+    hipLaunchKernelGGL((k_tiny_num<WW, KK>), dim3(round8((rows + 256 / (WW) - 1) / (256 / (WW)), 4096)), \
+                       dim3(256), 0, s, t)
+    switch (c) {
+    case 0: MHS_TINY(8, 1); break;
+    case 1: MHS_TINY(32, 1); break;
+    case 2: MHS_TINY(32, 2); break;
+    default: MHS_TINY(32, 4); break;
+    }
+#undef MHS_TINY
+}
+
 hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s,
                            int global_grid, hipStream_t side, hipEvent_t fork, hipEvent_t join) {
     if (M <= 0) return hipSuccess;
@@ -1922,6 +2038,9 @@ hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int
     a.bin = SYM_WAVE;
     hipLaunchKernelGGL(k_sym_wave<SYM_WAVE_BYTES>, dim3(round8((M + WPB - 1) / WPB, 2048)), dim3(256),
                        WPB * SYM_WAVE_BYTES, s, a);
+    a.bin = SYM_WM;
+    hipLaunchKernelGGL(k_sym_wave<SYM_WM_BYTES>, dim3(round8((M + WPB - 1) / WPB, 1024)), dim3(256),
+                       WPB * SYM_WM_BYTES, s, a);
     {
         TinyArgs t{};
         t.M = M;
@@ -1929,13 +2048,12 @@ hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int
         t.Acol = A.col;
         t.bmeta = w.bmeta;
         t.Bcol = B.col;
-        t.list = w.bin_list + (long long)(SYM_TINY - 1) * M;
         t.stats = w.stats;
         t.grp = w.grp;
         t.Cptr = Cptr;
         t.ctiles = w.ctiles;
-        hipLaunchKernelGGL((k_tiny<TINY_W, false>), dim3(round8((M + 256 / TINY_W - 1) / (256 / TINY_W), 2048)),
-                           dim3(256), 0, s, t);
+        t.list = w.bin_list + (long long)(SYM_TINY - 1) * M;
+        hipLaunchKernelGGL(k_tiny_sym, dim3(TINY_SYM_GRID * TINY_NC), dim3(256), 0, s, t);
     }
     if (side) {
         hipError_t e = hipEventRecord(join, side);
@@ -1951,7 +2069,7 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
     long long* part = (long long*)w.scan_part;
     hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.stats, w.blkflop, w.nflop);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.rflop, w.rlo, w.rhi,
-                       w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq);
+                       w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num);
 }
 
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
@@ -2003,23 +2121,24 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
         hipLaunchKernelGGL(k_num_wave<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
                            WPB * NUM_W16_BYTES, s, a);
     }
-    if (h.num_count[NUM_TINY] > 0) {
+    for (int c = TINY_NC - 1; c >= 0; --c) {
+        const int count = h.num_count[NUM_TINY + c];
+        if (count <= 0) continue;
         TinyArgs t{};
         t.M = A.M;
-        t.count = h.num_count[NUM_TINY];
+        t.count = count;
+        t.bin = NUM_TINY + c;
         t.Aptr = A.ptr;
         t.Acol = A.col;
         t.Aval = A.val;
         t.bmeta = w.bmeta;
         t.Bcol = B.col;
         t.Bval = B.val;
-        t.list = w.bin_list + (long long)(NUM_TINY - 1) * A.M;
+        t.list = w.bin_list + (long long)(t.bin - 1) * A.M;
         t.Cptr = Cptr;
         t.Ccol = Ccol;
         t.Cval = Cval;
-        const int teams = 256 / TINY_W;
-        hipLaunchKernelGGL((k_tiny<TINY_W, true>), dim3(round8((t.count + teams - 1) / teams, 4096)), dim3(256), 0,
-                           s, t);
+        launch_tiny_num(c, count, t, s);
     }
     if (h.num_count[NUM_W16G] > 0) {
         const int count = a.count = h.num_count[NUM_W16G];

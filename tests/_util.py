@@ -79,6 +79,8 @@ def bin_zoo(seed: int = 11):
         arows.append(list(range(s, s + 8)))
     for i in range(10):                              # scattered small: hash, wave
         arows.append(sorted(rng.choice(np.arange(1000, K - 1), 2, replace=False).tolist()))
+    for i in range(10):                              # scattered small-medium: hash, 16 KiB wave
+        arows.append(sorted(rng.choice(np.arange(1000, K - 1), 4, replace=False).tolist()))
     for i in range(6):                               # scattered medium: hash, 256-thread block
         arows.append(sorted(rng.choice(np.arange(1000, K - 1), 20, replace=False).tolist()))
     for i in range(4):                               # scattered large: 1024-thread block
@@ -176,4 +178,53 @@ def group_zoo(seed: int = 3, K: int = 6000, N: int = 30_000):
     Bptr[1:] = np.cumsum([len(r) for r in brows])
     Bc = np.concatenate(brows).astype(np.int32)
     Bv = rng.uniform(0.1, 1.0, len(Bc))
+    return (M, K, Aptr.astype(np.int32), Acol, Av), (K, N, Bptr.astype(np.int32), Bc, Bv)
+
+
+def tiny_zoo(seed: int = 7, K: int = 3000, N: int = 5000):
+    """Rows for every tiny class (team of W lanes x K products per lane: flop <= 8 with
+    nA <= 8, <= 32, <= 64, <= 128 with nA <= 32), with colliding columns (B rows drawn
+    from a narrow column window, repeated A entries) so segments of equal columns span
+    lanes and slots, plus rows just past the limits (flop 129+, nA 33+ with empty B rows)."""
+    rng = np.random.default_rng(seed)
+    brows = []
+    for k in range(K):
+        kind = k % 5
+        if kind == 0:
+            brows.append(np.zeros(0, np.int64))                                     # empty B row
+        elif kind == 1:
+            brows.append(np.unique(rng.integers(0, 200, int(rng.integers(1, 4)))))  # narrow: collisions
+        else:
+            brows.append(np.unique(rng.integers(0, N, int(rng.integers(1, 9)))))
+    Bptr = np.zeros(K + 1, np.int64)
+    Bptr[1:] = np.cumsum([len(r) for r in brows])
+    Bc = np.concatenate(brows).astype(np.int32)
+    Bv = rng.uniform(0.1, 1.0, len(Bc))
+    blen = np.diff(Bptr)
+    nonempty = np.nonzero(blen)[0]
+    empty = np.nonzero(blen == 0)[0]
+    arows = []
+    for target in (1, 4, 8, 20, 32, 50, 64, 100, 128, 129, 200):
+        for _ in range(40):
+            ks, f = [], 0
+            for _try in range(400):
+                if f >= target or len(ks) >= 32:
+                    break
+                k = int(rng.choice(nonempty))
+                if f + blen[k] > target:
+                    continue
+                ks.append(k)
+                f += int(blen[k])
+                if rng.random() < 0.2 and f + blen[k] <= target and len(ks) < 32:
+                    ks.append(k)  # repeated A entry: every product collides
+                    f += int(blen[k])
+            arows.append(sorted(ks))
+    for _ in range(20):  # many A entries, few products: nA > 32 is not tiny
+        arows.append(sorted(rng.choice(empty, 34, replace=False).tolist() + [int(rng.choice(nonempty))]))
+    arows.append([])
+    M = len(arows)
+    Aptr = np.zeros(M + 1, np.int64)
+    Aptr[1:] = np.cumsum([len(r) for r in arows])
+    Acol = np.array([k for r in arows for k in r], np.int32)
+    Av = rng.uniform(0.1, 1.0, len(Acol))
     return (M, K, Aptr.astype(np.int32), Acol, Av), (K, N, Bptr.astype(np.int32), Bc, Bv)

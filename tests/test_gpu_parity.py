@@ -12,7 +12,7 @@ import pytest
 import mhspgemm
 from mhspgemm import synth
 from oracle import oracle as orc
-from _util import GOLDEN, PRODUCT_CASES, bin_zoo, group_zoo, load_golden, random_csr, run_zoo
+from _util import GOLDEN, PRODUCT_CASES, bin_zoo, group_zoo, load_golden, random_csr, run_zoo, tiny_zoo
 
 pytestmark = pytest.mark.gpu
 
@@ -89,6 +89,18 @@ def test_bin_zoo_every_bin(tool):
     # every symbolic bin (1..4) and numeric bin (1..5) saw rows
     assert all(t.sym_bins[i] > 0 for i in range(0, 5)), t.sym_bins
     assert all(t.num_bins[i] > 0 for i in range(0, 6)), t.num_bins
+
+
+@pytest.mark.parametrize("seed", [7, 8])
+def test_tiny_zoo_every_class(tool, seed):
+    (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = tiny_zoo(seed)
+    A = mhspgemm.CSR(M, K, Ap, Ac, Av)
+    B = mhspgemm.CSR(K2, N, Bp, Bc, Bv)
+    t = check(tool, A, B)
+    # every tiny class (symbolic bins 5..8, numeric bins 8..11) and the wave bin saw rows
+    assert all(t.sym_bins[i] > 0 for i in range(5, 9)), t.sym_bins
+    assert all(t.num_bins[i] > 0 for i in range(8, 12)), t.num_bins
+    assert t.num_bins[1] > 0, t.num_bins
 
 
 @pytest.mark.parametrize("seed", [5, 6])
