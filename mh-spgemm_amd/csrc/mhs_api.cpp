@@ -350,7 +350,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     w.asame = (unsigned char*)(ctx->ws + L.asame);
     w.grp = (unsigned char*)(ctx->ws + L.grp);
     w.groups = ctx->groups ? 1 : 0;
-    w.tiny_num = B->N <= TINY_NUM_NMAX ? 1 : 0;  // packed tiny sort keys hold the column in 24 bits
+    w.tiny_num = B->N <= TINY_NUM_NMAX ? 1 : 0;  // packed tiny sort keys hold the column in 23 bits
     w.bin_list = (int*)(ctx->ws + L.bin_list);
     w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
     w.nflop = M > 0 ? analyze_blocks(A->nnz, M) : 0;

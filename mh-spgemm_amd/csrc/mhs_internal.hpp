@@ -30,16 +30,23 @@ constexpr int SCAN_ITEMS = 1024;// rows per block in the row_ptr scan and the bi
 
 // Symbolic bins (by LDS need and tile work).
 // Tiny rows: a team of W lanes per row holding K products per lane (flop <= W*K,
-// nA <= W), sorted by column in registers -- no table, no LDS.  Classes, smallest
-// first; a row takes the first class it fits.
-constexpr int TINY_NC = 4;
-constexpr int TINY_EBITS = 7;              // numeric sort key = (column << 7) | element (W*K <= 128)
-constexpr int TINY_NUM_NMAX = 1 << 24;     // ... so the numeric tiny classes need N <= 2^24 columns
-__host__ __device__ constexpr int tiny_w(int c) { return c == 0 ? 8 : 32; }
-__host__ __device__ constexpr int tiny_k(int c) { return c <= 1 ? 1 : (c == 2 ? 2 : 4); }
-__host__ __device__ inline int tiny_class(int flop, int nA) {
+// nA <= W), sorted by column in registers -- no table (numeric parks the values in
+// LDS by element during the sort).  Classes, smallest first; a row takes the first
+// class it fits: (8,1) (32,1) (32,2) (32,4) (64,4) (64,8).
+constexpr int TINY_NC = 6;
+constexpr int TINY_EBITS = 9;              // numeric sort key = (column << 9) | element (W*K <= 512)
+constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so the numeric tiny classes need N < 2^23 - 1 columns
+__host__ __device__ constexpr int tiny_w(int c) { return c == 0 ? 8 : c <= 3 ? 32 : 64; }
+__host__ __device__ constexpr int tiny_k(int c) { return c <= 1 ? 1 : c == 2 ? 2 : c <= 4 ? 4 : 8; }
+// Symbolic uses the classes below TINY_SYM_NC only (past 128 products a hash table
+// counts faster than a sort); numeric uses the 64-lane classes for rows whose table
+// would not fit the small wave bin (measured: cop20k-like 2.3x slower sorted, while
+// rows that need big tables run 2x faster sorted).
+constexpr int TINY_SYM_NC = 4;
+constexpr int TINY_NUM_SMALL = 4;  // numeric classes >= this only replace big-table rows
+__host__ __device__ inline int tiny_class(int flop, int nA, int nc = TINY_NC) {
     if (flop <= 0) return -1;
-    for (int c = 0; c < TINY_NC; ++c)
+    for (int c = 0; c < nc; ++c)
         if (flop <= tiny_w(c) * tiny_k(c) && nA <= tiny_w(c)) return c;
     return -1;
 }
@@ -53,7 +60,10 @@ enum SymBin : int {
 // column pattern, processed together by one wave: every B value loaded feeds R rows).
 enum NumBin : int {
     NUM_NONE = 0, NUM_WS = 1, NUM_W16 = 2, NUM_B256 = 3, NUM_B1024 = 4, NUM_GLOBAL = 5, NUM_WSG = 6,
-    NUM_W16G = 7, NUM_TINY = 8, NUM_NB = NUM_TINY + TINY_NC
+    NUM_W16G = 7, NUM_TINY = 8,
+    NUM_WSH = NUM_TINY + TINY_NC,  // NUM_WS / NUM_W16 rows in hash mode (their own kernels: see MODES)
+    NUM_W16H,
+    NUM_NB
 };
 // Row groups: rows i-1, i of A with the same column pattern (FEM dofs of one node)
 // have C rows with one pattern.  Maximal runs are broken every RG_BREAK rows and cut
@@ -176,7 +186,11 @@ __host__ __device__ inline bool mcached(int span, int tflop) { return span <= MC
 __host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_max) {
     if (span <= dense_span_max) return NM_DENSE;
     if (span <= RMAP_SPAN_MAX) return NM_RMAP;
-    return num_need_direct(span, n) <= num_need_hash(t, n) ? NM_DIRECT : NM_HASH;
+    // direct-mapped (no probes, no tile sort) unless it needs more LDS than a hash table
+    // at load 1/2 would: the tighter hash sizing only shrinks the rows that hash anyway
+    const long long hash_half = (long long)next_pow2(2 * (t < 1 ? 1 : t)) * 16 +
+                                align16((long long)(n > next_pow2(t) ? n : next_pow2(t)) * 8);
+    return num_need_direct(span, n) <= hash_half ? NM_DIRECT : NM_HASH;
 }
 __host__ __device__ inline long long num_need(int span, int t, int n, int dense_span_max) {
     const int m = num_mode(span, t, n, dense_span_max);

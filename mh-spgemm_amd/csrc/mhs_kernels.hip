@@ -358,6 +358,43 @@ __device__ void team_bitonic(const Team& tm, unsigned long long* S, int P) {
     }
 }
 
+// Bitonic sort of W*K unsigned keys held by a team of W lanes, K per lane, ascending
+// over element e = i*W + tl (slot i, team lane tl): partners at distance d < W are in
+// other lanes (shuffles), at d >= W in other slots of the lane.  Compare-exchange by
+// selects (no divergent branches).
+template <int W, int K>
+__device__ __forceinline__ void reg_bitonic(unsigned (&key)[K], int tl) {
+#pragma unroll
+    for (int k = 2; k <= W * K; k <<= 1) {
+#pragma unroll
+        for (int d = k >> 1; d > 0; d >>= 1) {
+            if (d < W) {
+                unsigned ok[K];
+#pragma unroll
+                for (int i = 0; i < K; ++i) ok[i] = (unsigned)__shfl_xor((int)key[i], d, W);
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const bool asc = ((i * W + tl) & k) == 0, low = (tl & d) == 0;
+                    const bool take = (low == asc) ? ok[i] < key[i] : ok[i] > key[i];
+                    key[i] = take ? ok[i] : key[i];
+                }
+            } else {
+                const int ds = d / W;
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    if (i & ds) continue;
+                    const int j = i | ds;
+                    const bool asc = ((i * W + tl) & k) == 0;
+                    const unsigned lo_ = key[i] < key[j] ? key[i] : key[j];
+                    const unsigned hi_ = key[i] < key[j] ? key[j] : key[i];
+                    key[i] = asc ? lo_ : hi_;
+                    key[j] = asc ? hi_ : lo_;
+                }
+            }
+        }
+    }
+}
+
 template <bool GLOBALMEM>
 __device__ __forceinline__ void acc_add(double* p, double v) {
     if constexpr (GLOBALMEM) unsafeAtomicAdd(p, v);
@@ -532,7 +569,7 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
         rlo[row] = lo;
         rhi[row] = hi;
         const int nA = Aptr[row + 1] - Aptr[row];
-        const int tc = tiny_class(f, nA);
+        const int tc = tiny_class(f, nA, TINY_SYM_NC);
         const int bin = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
         if (bin == SYM_NONE) {
@@ -1106,9 +1143,14 @@ struct Accum {
                 s = tc - lo;
             } else {
                 s = hslot(tc, hshift);
-                while (E[s].key != tc) s = (s + 1) & (H - 1);
             }
-            const uint4 q = *reinterpret_cast<const uint4*>(&E[s]);  // one ds_read_b128
+            uint4 q = *reinterpret_cast<const uint4*>(&E[s]);  // one ds_read_b128: mask, base, key
+            if constexpr (MODE == NM_HASH) {
+                while ((int)q.w != tc) {
+                    s = (s + 1) & (H - 1);
+                    q = *reinterpret_cast<const uint4*>(&E[s]);
+                }
+            }
             const unsigned long long mask = ((unsigned long long)q.y << 32) | q.x;
             const unsigned long long below = (1ull << (x.c & (TILE_BITS - 1))) - 1;
             idx = (int)q.z + __popcll(mask & below);
@@ -1346,10 +1388,12 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
                                           int dense_span_max, int nA, bool tiny_ok) {
     if (n == 0) return NUM_NONE;
     const int tc = tiny_ok ? tiny_class(flop, nA) : -1;
-    if (tc >= 0) return NUM_TINY + tc;
+    if (tc >= 0 && tc < TINY_NUM_SMALL) return NUM_TINY + tc;
     const long long need = num_need(span, t, n, dense_span_max);
-    if (need <= NUM_WS_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WS;
-    if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16;
+    const bool hash = num_mode(span, t, n, dense_span_max) == NM_HASH;
+    if (need <= NUM_WS_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return hash ? NUM_WSH : NUM_WS;
+    if (tc >= 0) return NUM_TINY + tc;  // a bigger table than the small wave bin's: sort in registers
+    if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return hash ? NUM_W16H : NUM_W16;
     if (need <= NUM_B256_BYTES - BLOCK_HDR && flop <= NUM_B256_WORK) return NUM_B256;
     if (need <= B1024_BYTES) return NUM_B1024;
     atomicMax(gneed, (int)(need > INT_MAX ? INT_MAX : need));
@@ -1359,7 +1403,8 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
 // Grouped numeric bin of a group of R rows (NUM_NONE: run its rows one by one).
 __device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t, int R, int dense_span_max,
                                                 int nA, bool tiny_ok) {
-    if (R < 2 || n == 0 || (tiny_ok && tiny_class(flop, nA) >= 0)) return NUM_NONE;  // tiny rows: one by one
+    if (R < 2 || n == 0 || (tiny_ok && tiny_class(flop, nA, TINY_NUM_SMALL) >= 0))
+        return NUM_NONE;  // tiny rows: one by one
     const long long need = num_need_rows(span, t, n, dense_span_max, R);
     if (need <= NUM_WSG_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WSG;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16G;
@@ -1630,7 +1675,14 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
 
 // Row-level scalars are made provably wave-uniform (readfirstlane) so that the
 // mode dispatch and every per-row loop bound compile to scalar control flow.
-template <class Team, bool GLOBALMEM, bool GROUPED = false>
+// MODES: which row bodies a kernel instantiates (the binning sends a row only to a
+// kernel that has its mode): the hash body's register sort would otherwise set the
+// register budget -- and the occupancy -- of the direct-mapped wave kernels too.
+enum NumModes : int { MODES_ALL = 0, MODES_NOHASH = 1, MODES_HASH = 2 };
+
+// Row-level scalars are made provably wave-uniform (readfirstlane) so that the
+// mode dispatch and every per-row loop bound compile to scalar control flow.
+template <class Team, bool GLOBALMEM, bool GROUPED = false, int MODES = MODES_ALL>
 __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region, int* counter,
                         int4* stage, int R = 1) {
     const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
@@ -1642,17 +1694,21 @@ __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region,
     const int a0 = __builtin_amdgcn_readfirstlane(a.Aptr[row]);
     const int a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
     const int mode = num_mode(span, t, n, a.dense_span_max);
+    if constexpr (MODES == MODES_HASH) {
+        num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
+        return;
+    }
     if (mode == NM_DENSE)
         num_row_body<Team, GLOBALMEM, NM_DENSE, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else if (mode == NM_RMAP)
         num_row_body<Team, GLOBALMEM, NM_RMAP, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
-    else if (mode == NM_DIRECT)
+    else if (MODES == MODES_NOHASH || mode == NM_DIRECT)
         num_row_body<Team, GLOBALMEM, NM_DIRECT, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else
         num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
 }
 
-template <int BYTES, bool GROUPED = false>
+template <int BYTES, bool GROUPED = false, bool HASH = false>
 __global__ __launch_bounds__(256, MHS_NUM_WAVES_EU) void k_num_wave(NumArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int w = threadIdx.x >> 6;
@@ -1661,10 +1717,11 @@ __global__ __launch_bounds__(256, MHS_NUM_WAVES_EU) void k_num_wave(NumArgs a) {
     for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride) {
         const int row = __builtin_amdgcn_readfirstlane(a.list[rw.first]);
         if constexpr (GROUPED)  // a group head: R rows of one pattern
-            num_row<WaveTeam, false, true>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
-                                           __builtin_amdgcn_readfirstlane((int)a.grp[row]));
+            num_row<WaveTeam, false, true, MODES_ALL>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
+                                                         __builtin_amdgcn_readfirstlane((int)a.grp[row]));
         else
-            num_row<WaveTeam, false>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr);
+            num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH>(tm, a, row, reg + WAVE_HDR,
+                                                                             (int*)reg, nullptr);
     }
 }
 
@@ -1710,7 +1767,6 @@ struct TinyArgs {
 template <int W, int K, bool NUMERIC>
 __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
     static_assert((W & (W - 1)) == 0 && W <= 64 && (K & (K - 1)) == 0 && W * K <= (1 << TINY_EBITS), "team shape");
-    constexpr int LW = W == 8 ? 3 : W == 16 ? 4 : W == 32 ? 5 : 6;
     const int lane = lane_id();
     const int tl = lane & (W - 1);   // lane in the team
     const int tb = lane & ~(W - 1);  // the team's first lane
@@ -1718,6 +1774,8 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
     const unsigned long long below = tmask & lanemask_lt();
     const int count = NUMERIC ? a.count : a.stats->sym_count[a.bin];
     const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W), bid, nb);
+    extern __shared__ __attribute__((aligned(16))) char tiny_smem[];
+    double* vstage = (double*)tiny_smem + (size_t)(threadIdx.x / W) * (W * K);  // numeric: W*K doubles per team
     // the wave iterates while any of its teams has a row (shuffles need every lane)
     for (int it = rw.first; __ballot(it < rw.end) != 0; it += rw.stride) {
         const bool live = it < rw.end;
@@ -1741,9 +1799,11 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
         const int flop = __shfl(incl, tb + W - 1);
         const int excl = incl - len;
         // sort keys: symbolic the column; numeric (column << TINY_EBITS) | element, the
-        // value stays with its element and is fetched once after the sort
+        // value parked in the team's LDS slice at its element and fetched after the sort
         unsigned key[K];
-        double v[K];
+        int q[K];
+        bool valid[K];
+        double avs[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             const int p = i * W + tl;
@@ -1753,69 +1813,39 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
                 const int x = __shfl(incl, tb + j + step - 1);
                 j += x <= p ? step : 0;
             }
-            const bool valid = p < flop;
-            const int src = tb + (valid ? j : 0);
+            valid[i] = p < flop;
+            const int src = tb + (valid[i] ? j : 0);
             const int stj = __shfl(st, src);
             const int exj = __shfl(excl, src);
-            const double avj = NUMERIC ? __shfl(av, src) : 0.0;  // shuffles outside the branch: every lane
-            key[i] = 0xFFFFFFFFu;
-            v[i] = 0.0;
-            if (valid) {
-                const int q = stj + (p - exj);
-                const unsigned c = (unsigned)a.Bcol[q];
-                key[i] = NUMERIC ? (c << TINY_EBITS) | (unsigned)p : c;
-                if (NUMERIC) v[i] = avj * a.Bval[q];
-            }
+            avs[i] = NUMERIC ? __shfl(av, src) : 0.0;  // shuffles outside any branch: every lane
+            q[i] = valid[i] ? stj + (p - exj) : 0;      // clamped: every slot's loads issue together
         }
-        // bitonic sort of the keys, ascending, over e = i*W + tl (compare-exchange by selects)
+        int bc[K];
+        double bv[K];
 #pragma unroll
-        for (int k = 2; k <= W * K; k <<= 1) {
-#pragma unroll
-            for (int d = k >> 1; d > 0; d >>= 1) {
-                if (d < W) {
-                    unsigned ok[K];
-#pragma unroll
-                    for (int i = 0; i < K; ++i) ok[i] = (unsigned)__shfl_xor((int)key[i], d, W);
-#pragma unroll
-                    for (int i = 0; i < K; ++i) {
-                        const bool asc = ((i * W + tl) & k) == 0, low = (tl & d) == 0;
-                        const bool take = (low == asc) ? ok[i] < key[i] : ok[i] > key[i];
-                        key[i] = take ? ok[i] : key[i];
-                    }
-                } else {
-                    const int ds = d / W;
-#pragma unroll
-                    for (int i = 0; i < K; ++i) {
-                        if (i & ds) continue;
-                        const int j = i | ds;
-                        const bool asc = ((i * W + tl) & k) == 0;
-                        const unsigned lo_ = key[i] < key[j] ? key[i] : key[j];
-                        const unsigned hi_ = key[i] < key[j] ? key[j] : key[i];
-                        key[i] = asc ? lo_ : hi_;
-                        key[j] = asc ? hi_ : lo_;
-                    }
-                }
-            }
+        for (int i = 0; i < K; ++i) {
+            bc[i] = a.Bcol[q[i]];
+            if (NUMERIC) bv[i] = a.Bval[q[i]];
         }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const unsigned c = (unsigned)bc[i];
+            key[i] = !valid[i] ? 0xFFFFFFFFu : NUMERIC ? (c << TINY_EBITS) | (unsigned)(i * W + tl) : c;
+            if (NUMERIC) vstage[i * W + tl] = avs[i] * bv[i];
+        }
+        reg_bitonic<W, K>(key, tl);
         int c[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) c[i] = key[i] == 0xFFFFFFFFu ? INT_MAX : (int)(NUMERIC ? key[i] >> TINY_EBITS : key[i]);
+        double v[K];
         if constexpr (NUMERIC) {  // each sorted slot fetches its element's value
-            double vs[K];
+            wave_sync();
 #pragma unroll
             for (int i = 0; i < K; ++i) {
                 const int e = (int)(key[i] & ((1u << TINY_EBITS) - 1));
-                const int srcl = tb + (e & (W - 1)), slot = e >> LW;
-                double x = 0.0;
-#pragma unroll
-                for (int s2 = 0; s2 < K; ++s2) {
-                    const double y = __shfl(v[s2], srcl);
-                    x = slot == s2 ? y : x;
-                }
-                vs[i] = c[i] == INT_MAX ? 0.0 : x;
+                v[i] = c[i] == INT_MAX ? 0.0 : vstage[e];
             }
-#pragma unroll
-            for (int i = 0; i < K; ++i) v[i] = vs[i];
+            wave_sync();  // the slice is rewritten by the team's next row
         }
         // heads: element e differs from e-1 (slot i lane tl-1, or slot i-1 lane W-1)
         bool head[K];
@@ -1883,9 +1913,10 @@ __global__ __launch_bounds__(256) void k_tiny_num(TinyArgs a) {
 constexpr int TINY_SYM_GRID = 1024;
 __global__ __launch_bounds__(256) void k_tiny_sym(TinyArgs a) {
     const int c = (int)blockIdx.x / TINY_SYM_GRID, bid = (int)blockIdx.x % TINY_SYM_GRID;
-    static_assert(TINY_NC == 4 && tiny_w(0) == 8 && tiny_k(0) == 1 && tiny_w(1) == 32 && tiny_k(1) == 1 &&
-                      tiny_w(2) == 32 && tiny_k(2) == 2 && tiny_w(3) == 32 && tiny_k(3) == 4,
-                  "k_tiny_sym / launch_tiny instantiate the classes of tiny_class()");
+    static_assert(TINY_NC == 6 && tiny_w(0) == 8 && tiny_k(0) == 1 && tiny_w(1) == 32 && tiny_k(1) == 1 &&
+                      tiny_w(2) == 32 && tiny_k(2) == 2 && tiny_w(3) == 32 && tiny_k(3) == 4 &&
+                      tiny_w(4) == 64 && tiny_k(4) == 4 && tiny_w(5) == 64 && tiny_k(5) == 8 && TINY_SYM_NC == 4,
+                  "k_tiny_sym / launch_tiny_num instantiate the classes of tiny_class()");
     a.bin = SYM_TINY + c;
     a.list += (long long)c * a.M;
     switch (c) {
@@ -1973,6 +2004,9 @@ hipError_t init_kernel_attributes() {
         e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 LDS_MAX);
     if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     return e;
@@ -1987,12 +2021,14 @@ size_t sym_global_bytes_per_block(int N) {
 static void launch_tiny_num(int c, int rows, const TinyArgs& t, hipStream_t s) {
 #define MHS_TINY(WW, KK)                                                                                  \
     hipLaunchKernelGGL((k_tiny_num<WW, KK>), dim3(round8((rows + 256 / (WW) - 1) / (256 / (WW)), 4096)), \
-                       dim3(256), 0, s, t)
+                       dim3(256), 256 * (KK) * 8, s, t)
     switch (c) {
     case 0: MHS_TINY(8, 1); break;
     case 1: MHS_TINY(32, 1); break;
     case 2: MHS_TINY(32, 2); break;
-    default: MHS_TINY(32, 4); break;
+    case 3: MHS_TINY(32, 4); break;
+    case 4: MHS_TINY(64, 4); break;
+    default: MHS_TINY(64, 8); break;
     }
 #undef MHS_TINY
 }
@@ -2053,7 +2089,7 @@ hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int
         t.Cptr = Cptr;
         t.ctiles = w.ctiles;
         t.list = w.bin_list + (long long)(SYM_TINY - 1) * M;
-        hipLaunchKernelGGL(k_tiny_sym, dim3(TINY_SYM_GRID * TINY_NC), dim3(256), 0, s, t);
+        hipLaunchKernelGGL(k_tiny_sym, dim3(TINY_SYM_GRID * TINY_SYM_NC), dim3(256), 0, s, t);
     }
     if (side) {
         hipError_t e = hipEventRecord(join, side);
@@ -2114,6 +2150,18 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
         const int count = a.count = h.num_count[NUM_B256];
         a.list = w.bin_list + (long long)(NUM_B256 - 1) * A.M;
         hipLaunchKernelGGL((k_num_block<256, false>), dim3(round8(count, 1024)), dim3(256), NUM_B256_BYTES, s, a);
+    }
+    if (h.num_count[NUM_W16H] > 0) {
+        const int count = a.count = h.num_count[NUM_W16H];
+        a.list = w.bin_list + (long long)(NUM_W16H - 1) * A.M;
+        hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, false, true>), dim3(round8((count + WPB - 1) / WPB, 2048)),
+                           dim3(256), WPB * NUM_W16_BYTES, s, a);
+    }
+    if (h.num_count[NUM_WSH] > 0) {
+        const int count = a.count = h.num_count[NUM_WSH];
+        a.list = w.bin_list + (long long)(NUM_WSH - 1) * A.M;
+        hipLaunchKernelGGL((k_num_wave<NUM_WS_BYTES, false, true>),
+                           dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)), dim3(256), WPB * NUM_WS_BYTES, s, a);
     }
     if (h.num_count[NUM_W16] > 0) {
         const int count = a.count = h.num_count[NUM_W16];

@@ -81,6 +81,13 @@ def bin_zoo(seed: int = 11):
         arows.append(sorted(rng.choice(np.arange(1000, K - 1), 2, replace=False).tolist()))
     for i in range(10):                              # scattered small-medium: hash, 16 KiB wave
         arows.append(sorted(rng.choice(np.arange(1000, K - 1), 4, replace=False).tolist()))
+    for nb in (1, 3, 6, 9):                          # scattered rows of 50..450 products (tiny classes)
+        for i in range(4):
+            arows.append(sorted(rng.choice(np.arange(1000, K - 1), nb, replace=False).tolist()))
+    for i in range(4):                               # > 512 products, 50 tiles: hash, wave
+        arows.append([int(rng.integers(1000, K - 1))] * 12)
+    for i in range(4):                               # > 512 products, ~300 tiles: hash, 16 KiB wave
+        arows.append(sorted(rng.choice(np.arange(1000, K - 1), 6, replace=False).tolist() * 2))
     for i in range(6):                               # scattered medium: hash, 256-thread block
         arows.append(sorted(rng.choice(np.arange(1000, K - 1), 20, replace=False).tolist()))
     for i in range(4):                               # scattered large: 1024-thread block
@@ -183,9 +190,10 @@ def group_zoo(seed: int = 3, K: int = 6000, N: int = 30_000):
 
 def tiny_zoo(seed: int = 7, K: int = 3000, N: int = 5000):
     """Rows for every tiny class (team of W lanes x K products per lane: flop <= 8 with
-    nA <= 8, <= 32, <= 64, <= 128 with nA <= 32), with colliding columns (B rows drawn
-    from a narrow column window, repeated A entries) so segments of equal columns span
-    lanes and slots, plus rows just past the limits (flop 129+, nA 33+ with empty B rows)."""
+    nA <= 8; <= 32, 64, 128 with nA <= 32; <= 256, 512 with nA <= 64), with colliding
+    columns (B rows drawn from a narrow column window, repeated A entries) so segments of
+    equal columns span lanes and slots, plus rows just past the limits (flop 513+, nA
+    past the lane count with empty B rows)."""
     rng = np.random.default_rng(seed)
     brows = []
     for k in range(K):
@@ -204,23 +212,25 @@ def tiny_zoo(seed: int = 7, K: int = 3000, N: int = 5000):
     nonempty = np.nonzero(blen)[0]
     empty = np.nonzero(blen == 0)[0]
     arows = []
-    for target in (1, 4, 8, 20, 32, 50, 64, 100, 128, 129, 200):
-        for _ in range(40):
+    for target, amax in ((1, 8), (4, 8), (8, 8), (20, 32), (32, 32), (50, 32), (64, 32), (100, 32), (128, 32),
+                         (129, 32), (200, 64), (256, 64), (300, 64), (512, 64), (513, 64), (700, 64)):
+        for _ in range(30):
             ks, f = [], 0
-            for _try in range(400):
-                if f >= target or len(ks) >= 32:
+            for _try in range(600):
+                if f >= target or len(ks) >= amax:
                     break
                 k = int(rng.choice(nonempty))
                 if f + blen[k] > target:
                     continue
                 ks.append(k)
                 f += int(blen[k])
-                if rng.random() < 0.2 and f + blen[k] <= target and len(ks) < 32:
+                if rng.random() < 0.2 and f + blen[k] <= target and len(ks) < amax:
                     ks.append(k)  # repeated A entry: every product collides
                     f += int(blen[k])
             arows.append(sorted(ks))
-    for _ in range(20):  # many A entries, few products: nA > 32 is not tiny
-        arows.append(sorted(rng.choice(empty, 34, replace=False).tolist() + [int(rng.choice(nonempty))]))
+    for na in (34, 66):  # many A entries, few products: past a class's lane count
+        for _ in range(15):
+            arows.append(sorted(rng.choice(empty, na, replace=False).tolist() + [int(rng.choice(nonempty))]))
     arows.append([])
     M = len(arows)
     Aptr = np.zeros(M + 1, np.int64)
