@@ -86,7 +86,8 @@ constexpr int NUM_WSG_BYTES = 10240;  // grouped rows: 4 waves x 10 KiB = 40 KiB
 constexpr int NUM_B256_BYTES = 65536;
 constexpr int NUM_B256_WORK = 1 << 22;
 constexpr int LDS_MAX = 163840;         // gfx950: 160 KiB per workgroup (probed on the box)
-constexpr int BLOCK_HDR = 2048;         // per-block LDS header: reductions, counter, A-entry stage
+constexpr int STAGE_SUBS = 4;           // block kernels stage up to 4 x 64 A entries per barrier
+constexpr int BLOCK_HDR = 1024 + STAGE_SUBS * 65 * 16;  // per-block LDS header: reductions, counter, A-entry stage
 constexpr int WAVE_HDR = 16;            // per-wave LDS header
 constexpr int B1024_BYTES = LDS_MAX - BLOCK_HDR - 1024;  // budget of the 1024-thread kernels
 

@@ -406,19 +406,18 @@ __device__ __forceinline__ void acc_add(double* p, double v) {
 // a forward segmented OR scan collects each run's bits, the run's last lane
 // (tail) writes (tile, mask) at row_start + run index.  A run that crosses a
 // chunk edge is carried in `carry`.  Also checks the sorted-columns precondition.
+// One B row by a lane group of G lanes (every lane of the wave calls it: shuffles and
+// ballots); `valid` false for groups without a row.
 template <int G>
-__global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __restrict__ ptr,
-                                                const int* __restrict__ col, int* __restrict__ btcol,
-                                                unsigned long long* __restrict__ btmask,
-                                                int4* __restrict__ bmeta, int* __restrict__ bhi,
-                                                Stats* __restrict__ stats) {
+__device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* __restrict__ ptr,
+                                         const int* __restrict__ col, int* __restrict__ btcol,
+                                         unsigned long long* __restrict__ btmask, int4* __restrict__ bmeta,
+                                         int* __restrict__ bhi, int& err) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
     unsigned long long gmask = ~0ull;
     if constexpr (G < 64) gmask = ((1ull << G) - 1) << gbase;
-    const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
-    const bool valid = row < MB;
     const int s = valid ? ptr[row] : 0;
     const int e = valid ? ptr[row + 1] : 0;
     // same column pattern as the previous row (FEM dofs of one node): later
@@ -426,7 +425,7 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
     const int ps = (valid && row > 0) ? ptr[row - 1] : 0;
     const bool same_len = valid && row > 0 && e > s && (s - ps) == (e - s);
     bool differ = false;
-    int ntiles = 0, prev_col = -1, err = 0;
+    int ntiles = 0, prev_col = -1;
     unsigned long long carry = 0;
     for (int b = s; b < e; b += G) {
         const int j = b + gl;
@@ -475,6 +474,36 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
         bmeta[row] = make_int4(s, e - s, ntiles | (same ? SAME_PATTERN : 0), e > s ? (col[s] >> TILE_SHIFT) : INT_MAX);
         bhi[row] = e > s ? (col[e - 1] >> TILE_SHIFT) : -1;
     }
+}
+
+// G lanes per B row.  Per chunk of G entries: head = first entry of a tile run,
+// a forward segmented OR scan collects each run's bits, the run's last lane
+// (tail) writes (tile, mask) at row_start + run index.  A run that crosses a
+// chunk edge is carried in `carry`.  Also checks the sorted-columns precondition.
+// Rows longer than MASK_LONG chunks (power-law matrices) are deferred and then
+// walked by the whole wave, one at a time: a G-lane group would hold its wave (and
+// the kernel's tail) for thousands of iterations.
+constexpr int MASK_LONG = 16;
+template <int G>
+__global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __restrict__ ptr,
+                                                const int* __restrict__ col, int* __restrict__ btcol,
+                                                unsigned long long* __restrict__ btmask,
+                                                int4* __restrict__ bmeta, int* __restrict__ bhi,
+                                                Stats* __restrict__ stats) {
+    const int lane = lane_id();
+    const int gl = lane & (G - 1);
+    const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
+    const bool valid = row < MB;
+    int err = 0;
+    bool lng = false;
+    if constexpr (G < 64) lng = valid && ptr[row + 1] - ptr[row] > MASK_LONG * G;
+    mask_row<G>(row, valid && !lng, N, ptr, col, btcol, btmask, bmeta, bhi, err);
+    if constexpr (G < 64) {
+        for (unsigned long long lb = __ballot(lng && gl == 0); lb; lb &= lb - 1) {
+            const int r = __shfl(row, __builtin_ctzll(lb));
+            mask_row<64>(r, true, N, ptr, col, btcol, btmask, bmeta, bhi, err);
+        }
+    }
     if (__any(err != 0)) {
         int werr = err;
 #pragma unroll
@@ -509,23 +538,19 @@ __device__ bool last_block_done(int* done) {
     return last;
 }
 
+// One A row by a group of G lanes (all lanes of the wave call it); returns the row's
+// flop in every lane of the group (0 for invalid groups).
 template <int G>
-__global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __restrict__ Aptr,
-                                                 const int* __restrict__ Acol,
-                                                 const int4* __restrict__ bmeta,
+__device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, const int* __restrict__ Aptr,
+                                                 const int* __restrict__ Acol, const int4* __restrict__ bmeta,
                                                  const int* __restrict__ bhi, int* __restrict__ rflop,
                                                  int* __restrict__ rtflop, int* __restrict__ rlo,
                                                  int* __restrict__ rhi, int* __restrict__ ctiles,
                                                  unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
-                                                 unsigned long long* __restrict__ blkflop,
-                                                 unsigned char* __restrict__ asame,
-                                                 Stats* __restrict__ stats) {
-    const int lane = lane_id();
-    const int gl = lane & (G - 1);
-    const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
-    const bool valid = row < M;
+                                                 unsigned char* __restrict__ asame, int& err) {
+    const int gl = lane_id() & (G - 1);
     long long flop = 0, tflop = 0;
-    int lo = INT_MAX, hi = -1, err = 0;
+    int lo = INT_MAX, hi = -1;
     bool differ = true;  // row's column pattern differs from row-1's (row groups)
     if (valid) {
         const int s = Aptr[row], e = Aptr[row + 1];
@@ -557,11 +582,8 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
         const int od = __shfl_xor((int)differ, d);  // every lane shuffles (no short circuit)
         differ = differ || od != 0;
     }
-    if (valid && gl == 0) asame[row] = (unsigned char)(differ ? 0 : 1);
-#ifdef MHS_DEBUG_PRINT
-    if (valid && M < 16) printf("row %d gl %d differ %d\n", row, gl, (int)differ);
-#endif
     if (valid && gl == 0) {
+        asame[row] = (unsigned char)(differ ? 0 : 1);
         const int f = sat_int(flop), tf = sat_int(tflop);
         const int span = f ? hi - lo + 1 : 0;
         rflop[row] = f;
@@ -577,9 +599,44 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
             ctiles[row] = 0;
         }
     }
+    return valid ? flop : 0;
+}
+
+// G lanes per A row; rows longer than AN_LONG*G entries are deferred to whole-wave
+// walks (as in k_mask_b).
+constexpr int AN_LONG = 16;
+template <int G>
+__global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __restrict__ Aptr,
+                                                 const int* __restrict__ Acol,
+                                                 const int4* __restrict__ bmeta,
+                                                 const int* __restrict__ bhi, int* __restrict__ rflop,
+                                                 int* __restrict__ rtflop, int* __restrict__ rlo,
+                                                 int* __restrict__ rhi, int* __restrict__ ctiles,
+                                                 unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
+                                                 unsigned long long* __restrict__ blkflop,
+                                                 unsigned char* __restrict__ asame,
+                                                 Stats* __restrict__ stats) {
+    const int lane = lane_id();
+    const int gl = lane & (G - 1);
+    const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
+    const bool valid = row < M;
+    int err = 0;
+    bool lng = false;
+    if constexpr (G < 64) lng = valid && Aptr[row + 1] - Aptr[row] > AN_LONG * G;
+    long long flop = analyze_row<G>(row, valid && !lng, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
+                                    ctiles, sym_bin, Cptr, asame, err);
+    flop = gl == 0 ? flop : 0;
+    if constexpr (G < 64) {
+        for (unsigned long long lb = __ballot(lng && gl == 0); lb; lb &= lb - 1) {
+            const int r = __shfl(row, __builtin_ctzll(lb));
+            const long long f = analyze_row<64>(r, true, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
+                                                ctiles, sym_bin, Cptr, asame, err);
+            flop += lane == 0 ? f : 0;
+        }
+    }
     // per-block flop partial (plain store; summed by the scan's last block)
     __shared__ unsigned long long wsum[4];
-    unsigned long long mine = (valid && gl == 0) ? (unsigned long long)flop : 0ull;
+    unsigned long long mine = (unsigned long long)flop;
     mine = wave_sum(mine);
     if (lane == 0) wsum[threadIdx.x >> 6] = mine;
     __syncthreads();
@@ -851,43 +908,56 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
                                              const double* __restrict__ Aval,
                                              const int4* __restrict__ bmeta, bool tiles, int Grow,
                                              const F& f, int4* stage) {
-    // stage[-1] = {visits, longest run, group width}; stage[e] = {B start, length, A index, run length}
-    for (int jb = a0; jb < a1; jb += 64) {
-        if (threadIdx.x < 64) {
-            const StagedChunk x = stage_chunk(threadIdx.x, jb, a1, Acol, nullptr, bmeta, tiles);
+    // Waves 0..S-1 each stage one 64-entry sub-chunk at once (their Acol -> bmeta load
+    // chains overlap; one barrier per 64*S A entries -- rows with thousands of short A
+    // entries were bound by one chunk's load chain per barrier).  Sub-chunk s:
+    // stage[s*65] = {visits, longest run, group width}; stage[s*65+1+e] = {B start,
+    // length, A index, run length}.
+    constexpr int S = (T / 64) < STAGE_SUBS ? (T / 64) : STAGE_SUBS;
+    const int wv = threadIdx.x >> 6;
+    for (int jr = a0; jr < a1; jr += 64 * S) {
+        if (wv < S) {
+            const int jb = jr + 64 * wv;
+            const int lane = lane_id();
+            int4* sg = stage + wv * 65;
+            const StagedChunk x = stage_chunk(lane, jb, a1, Acol, nullptr, bmeta, tiles);
             const int h = x.src;
             const int st = __shfl(x.st, h), ln = __shfl(x.ln, h), L = __shfl(x.L, h);
-            if (threadIdx.x < x.nh) stage[threadIdx.x] = make_int4(st, ln, jb + h, L);
+            if (lane < x.nh) sg[1 + lane] = make_int4(st, ln, jb + h, L);
             const int G = (F::kValues && x.lmax > 1 && Grow < MHS_RUN_GMIN) ? MHS_RUN_GMIN : Grow;
-            if (threadIdx.x == 0) stage[-1] = make_int4(x.nh, x.lmax, G, 0);
+            if (lane == 0) sg[0] = make_int4(jb < a1 ? x.nh : 0, x.lmax, G, 0);
         }
         __syncthreads();
-        const int4 hd = stage[-1];
-        const int nloc = hd.x, lmax = hd.y, G = hd.z;
-        const int gs = 31 - __clz(G);  // G is a power of two
-        const int grp = threadIdx.x >> gs, gl = threadIdx.x & (G - 1), ngrp = T >> gs;  // ngrp <= 64
-        const int iters = (nloc + ngrp - 1) / ngrp;
-        for (int it = 0; it < iters; ++it) {
-            const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
-            if (e >= nloc) continue;
-            const int4 v = stage[e];
-            if constexpr (F::kValues) {
-                if (lmax == 1) {
-                    const double a[1] = {Aval[v.z]};
-                    run_segment_run<1>(f, v.x, v.y, gl, G, a, 1);
-                } else if (lmax == 2) {
-                    const double a[2] = {Aval[v.z], Aval[v.z + (v.w > 1)]};
-                    run_segment_run<2>(f, v.x, v.y, gl, G, a, v.w);
-                } else if (lmax == 3) {
-                    const double a[3] = {Aval[v.z], Aval[v.z + (v.w > 1)], Aval[v.z + 2 * (v.w > 2)]};
-                    run_segment_run<3>(f, v.x, v.y, gl, G, a, v.w);
+        for (int sc = 0; sc < S; ++sc) {
+            const int4* sg = stage + sc * 65;
+            const int4 hd = sg[0];
+            const int nloc = hd.x, lmax = hd.y, G = hd.z;
+            if (nloc == 0) break;  // sub-chunks past the row's end are empty (and all later ones)
+            const int gs = 31 - __clz(G);  // G is a power of two
+            const int grp = threadIdx.x >> gs, gl = threadIdx.x & (G - 1), ngrp = T >> gs;  // ngrp <= 64
+            const int iters = (nloc + ngrp - 1) / ngrp;
+            for (int it = 0; it < iters; ++it) {
+                const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
+                if (e >= nloc) continue;
+                const int4 v = sg[1 + e];
+                if constexpr (F::kValues) {
+                    if (lmax == 1) {
+                        const double a[1] = {Aval[v.z]};
+                        run_segment_run<1>(f, v.x, v.y, gl, G, a, 1);
+                    } else if (lmax == 2) {
+                        const double a[2] = {Aval[v.z], Aval[v.z + (v.w > 1)]};
+                        run_segment_run<2>(f, v.x, v.y, gl, G, a, v.w);
+                    } else if (lmax == 3) {
+                        const double a[3] = {Aval[v.z], Aval[v.z + (v.w > 1)], Aval[v.z + 2 * (v.w > 2)]};
+                        run_segment_run<3>(f, v.x, v.y, gl, G, a, v.w);
+                    } else {
+                        const double a[4] = {Aval[v.z], Aval[v.z + (v.w > 1)], Aval[v.z + 2 * (v.w > 2)],
+                                             Aval[v.z + 3 * (v.w > 3)]};
+                        run_segment_run<4>(f, v.x, v.y, gl, G, a, v.w);
+                    }
                 } else {
-                    const double a[4] = {Aval[v.z], Aval[v.z + (v.w > 1)], Aval[v.z + 2 * (v.w > 2)],
-                                         Aval[v.z + 3 * (v.w > 3)]};
-                    run_segment_run<4>(f, v.x, v.y, gl, G, a, v.w);
+                    run_segment(f, v.x, v.y, gl, G, 0.0);
                 }
-            } else {
-                run_segment(f, v.x, v.y, gl, G, 0.0);
             }
         }
         __syncthreads();
