@@ -193,10 +193,17 @@ __host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_m
                                 align16((long long)(n > next_pow2(t) ? n : next_pow2(t)) * 8);
     return num_need_direct(span, n) <= hash_half ? NM_DIRECT : NM_HASH;
 }
+// Wide rows: hash-mode rows whose table would not fit the 256-thread kernel's 64 KiB run
+// in the 1024-thread kernel with windowed dense masks and global accumulation (measured:
+// for smaller tables the hash kernels' occupancy wins).
+__host__ __device__ inline bool num_wide(int span, int t, int n, int dense_span_max);
 __host__ __device__ inline long long num_need(int span, int t, int n, int dense_span_max) {
     const int m = num_mode(span, t, n, dense_span_max);
     return m == NM_DENSE ? num_need_dense(span) : m == NM_RMAP ? num_need_rmap(span, n)
                                                : m == NM_DIRECT ? num_need_direct(span, n) : num_need_hash(t, n);
+}
+__host__ __device__ inline bool num_wide(int span, int t, int n, int dense_span_max) {
+    return num_mode(span, t, n, dense_span_max) == NM_HASH && num_need_hash(t, n) > NUM_B256_BYTES - BLOCK_HDR;
 }
 // One row's accumulator bytes in mode m (16-aligned); a group of R rows needs the
 // tables once and R accumulators.

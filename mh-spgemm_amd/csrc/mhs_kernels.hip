@@ -1463,6 +1463,7 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
     const bool hash = num_mode(span, t, n, dense_span_max) == NM_HASH;
     if (need <= NUM_WS_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return hash ? NUM_WSH : NUM_WS;
     if (tc >= 0) return NUM_TINY + tc;  // a bigger table than the small wave bin's: sort in registers
+    if (num_wide(span, t, n, dense_span_max)) return NUM_B1024;  // windowed masks, global accumulation
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return hash ? NUM_W16H : NUM_W16;
     if (need <= NUM_B256_BYTES - BLOCK_HDR && flop <= NUM_B256_WORK) return NUM_B256;
     if (need <= B1024_BYTES) return NUM_B1024;
@@ -1745,6 +1746,110 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
 
 // Row-level scalars are made provably wave-uniform (readfirstlane) so that the
 // mode dispatch and every per-row loop bound compile to scalar control flow.
+// ------------------------------------------------------------ wide rows ---
+// Rows whose tile tables would not fit a wave (scattered over a wide column range,
+// e.g. power-law rows touching hub columns): no hash and no tile sort.  The block
+// walks the row's tile span in windows of WIDE_WT tiles; per window the LDS holds a
+// dense 64-bit mask per tile and a C-row base per 4 tiles (9 bytes per tile), and the
+// products accumulate straight into the row's slice of C.val with global FP64
+// atomics (zeroed first).  A product's rank = base4[g] + popcounts of the masks of
+// the tiles before it in its group of 4 + popc(mask & below(col)).
+constexpr int WIDE_WT = 16384;  // tiles per window: 1 M columns (masks 128 KiB + bases 16 KiB)
+static_assert(WIDE_WT * 9 <= B1024_BYTES, "a wide window fits the 1024-thread kernel's LDS");
+
+struct WideTiles {
+    static constexpr bool kValues = false;
+    unsigned long long* masks;
+    int w0, w1;
+    const int* __restrict__ btcol;
+    const unsigned long long* __restrict__ btmask;
+    struct Item {
+        int tc;
+        unsigned long long m;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{btcol[i], btmask[i]}; }
+    __device__ __forceinline__ void put(const Item& x, double) const {
+        if (x.tc >= w0 && x.tc < w1) atomicOr(&masks[x.tc - w0], x.m);
+    }
+};
+
+struct WideAccum {
+    static constexpr bool kValues = true;
+    const unsigned long long* masks;
+    const int* base4;
+    int w0, w1;
+    double* crow;  // C.val + c0
+    const int* __restrict__ Bcol;
+    const double* __restrict__ Bval;
+    struct Item {
+        int c;
+        double v;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{Bcol[i], Bval[i]}; }
+    __device__ __forceinline__ void put(const Item& x, double a) const { add(x.c, a * x.v); }
+    __device__ __forceinline__ int col(int i) const { return Bcol[i]; }
+    __device__ __forceinline__ double val(int i) const { return Bval[i]; }
+    __device__ __forceinline__ void add(int c, double v) const {
+        const int tc = c >> TILE_SHIFT;
+        if (tc < w0 || tc >= w1) return;
+        const int sl = tc - w0, g = sl >> 2;
+        int idx = base4[g];
+        for (int k = g << 2; k < sl; ++k) idx += __popcll(masks[k]);
+        idx += __popcll(masks[sl] & ((1ull << (c & (TILE_BITS - 1))) - 1));
+        unsafeAtomicAdd(&crow[idx], v);
+    }
+    template <int RM>
+    __device__ __forceinline__ void add_rows(int, const double (&)[RM], int, int) const {}
+};
+
+template <int T>
+__device__ void num_row_wide(const BlockTeam<T, false>& tm, const NumArgs& a, int row, int lo, int hi, int c0,
+                             int n, int a0, int a1, char* region, int4* stage) {
+    unsigned long long* masks = (unsigned long long*)region;
+    int* base4 = (int*)(region + (size_t)WIDE_WT * 8);
+    double* crow = a.Cval + c0;
+    const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
+    const int flop = __builtin_amdgcn_readfirstlane(a.rflop[row]);
+    for (int r = tm.rank(); r < n; r += T) crow[r] = 0.0;
+    __threadfence();  // the zeros are visible to the (memory-side) atomics below
+    int carry = 0;    // C entries in earlier windows
+    for (int w0 = lo; w0 <= hi; w0 += WIDE_WT) {
+        const int w1 = min(hi + 1, w0 + WIDE_WT), wt = w1 - w0;
+        for (int sl = tm.rank(); sl < wt; sl += T) masks[sl] = 0ull;
+        tm.sync();
+        walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop,
+                      WideTiles{masks, w0, w1, a.btcol, a.btmask}, stage);
+        tm.sync();
+        const int ng = (wt + 3) >> 2;
+        tm.exclusive_scan(
+            ng,
+            [&](int g) {
+                int c = 0;
+                for (int k = g << 2; k < min(wt, (g << 2) + 4); ++k) c += __popcll(masks[k]);
+                return c;
+            },
+            [&](int g, int v) { base4[g] = carry + v; });
+        tm.sync();
+        walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, flop,
+                      WideAccum{masks, base4, w0, w1, crow, a.Bcol, a.Bval}, stage);
+        // column indices of the window: a thread per group of 4 tiles (scattered rows
+        // hold a few bits per tile), bits in order
+        int wc = 0;
+        for (int g = tm.rank(); g < ng; g += T) {
+            int idx = base4[g];
+            for (int k = g << 2; k < min(wt, (g << 2) + 4); ++k) {
+                unsigned long long m = masks[k];
+                wc += __popcll(m);
+                while (m) {
+                    a.Ccol[c0 + idx++] = ((w0 + k) << TILE_SHIFT) + __builtin_ctzll(m);
+                    m &= m - 1;
+                }
+            }
+        }
+        carry += tm.sum(wc);  // (sum syncs: the masks are free for the next window)
+    }
+}
+
 // MODES: which row bodies a kernel instantiates (the binning sends a row only to a
 // kernel that has its mode): the hash body's register sort would otherwise set the
 // register budget -- and the occupancy -- of the direct-mapped wave kernels too.
@@ -1802,9 +1907,23 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
     char* reg = GLOBALMEM ? (a.gscratch + (long long)blockIdx.x * a.gbytes) : (smem + BLOCK_HDR);
     int* counter = (int*)(smem + 128);
     int4* stage = (int4*)(smem + 1024);
-    for (RowWalk rw(a.count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
-        num_row<BlockTeam<T, GLOBALMEM>, GLOBALMEM>(tm, a, __builtin_amdgcn_readfirstlane(a.list[rw.first]),
-                                                     reg, counter, stage);
+    for (RowWalk rw(a.count, 1, 0); rw.first < rw.end; rw.first += rw.stride) {
+        const int row = __builtin_amdgcn_readfirstlane(a.list[rw.first]);
+        if constexpr (T == 1024 && !GLOBALMEM) {
+            const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
+            const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
+            const int t = __builtin_amdgcn_readfirstlane(a.ctiles[row]);
+            const int c0 = __builtin_amdgcn_readfirstlane(a.Cptr[row]);
+            const int n = __builtin_amdgcn_readfirstlane(a.Cptr[row + 1]) - c0;
+            if (num_wide(hi - lo + 1, t, n, a.dense_span_max)) {
+                num_row_wide<T>(tm, a, row, lo, hi, c0, n, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
+                                __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]), reg, stage);
+                tm.sync();
+                continue;
+            }
+        }
+        num_row<BlockTeam<T, GLOBALMEM>, GLOBALMEM>(tm, a, row, reg, counter, stage);
+    }
 }
 
 // ------------------------------------------------------------- tiny rows ---

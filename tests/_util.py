@@ -50,11 +50,14 @@ def bin_zoo(seed: int = 11):
     rng = np.random.default_rng(seed)
     N = 2_000_000
     K = 3000
-    # B rows: 0..999 "band" (64 consecutive cols), 1000..2999 "scatter" (50 random cols), row 2999 single entry
+    # B rows: 0..499 tile [0, 32000) with 64 consecutive cols each, 500..999 "band" (64 consecutive
+    # cols, 1000 apart), 1000..2998 "scatter" (50 random cols), row 2999 single entry
     Brows, Bcols = [], []
     for k in range(K):
         if k == K - 1:
             cs = np.array([12345])
+        elif k < 500:                                # contiguous tiling of [0, 32000)
+            cs = np.arange(64 * k, 64 * k + 64)
         elif k < 1000:
             off = 1000 * k % (N - 64)
             cs = np.arange(off, off + 64)
@@ -95,6 +98,8 @@ def bin_zoo(seed: int = 11):
     for i in range(2):                               # scattered huge: global memory
         arows.append(sorted(rng.choice(np.arange(1000, K - 1), 400, replace=False).tolist()))
     arows.append([5] * 3000)                         # heavy work, tiny pattern (duplicates)
+    arows.append(list(range(0, 330)))                # 21120 contiguous columns, direct: global memory
+    arows.append(sorted(rng.choice(np.arange(1000, K - 1), 120, replace=False).tolist()))  # wide: 1024 block
     arows.append(sorted(rng.choice(np.arange(0, 1000), 200, replace=False).tolist()))  # wide banded
     arows.append(list(range(0, 1000, 3)))            # direct, large span
     M = len(arows)

@@ -25,3 +25,10 @@ for k, nm in enumerate(names):
     print(f"{nm:20s} {ph[heads, k].mean():10.0f} cycles/head")
 tot = ph[heads, :6].sum()
 print("sum cycles over heads %.3e ; numeric ms %.4f" % (tot, t.Numeric))
+# the slowest rows (top 1% by total cycles): where their time goes
+tot_r = ph[:, :6].sum(1)
+thr = np.percentile(tot_r[heads], 99)
+slow = heads & (tot_r >= thr)
+print("slowest 1%% rows: %d rows, mean total %.0f cycles" % (slow.sum(), tot_r[slow].mean()))
+for k, nm in enumerate(names):
+    print(f"  {nm:20s} {ph[slow, k].mean():10.0f} cycles/row")
