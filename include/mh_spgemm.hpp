@@ -227,6 +227,23 @@ inline void MH_spgemm(const CSR& A, CSR& B, CSR& C, Timing& timing, Tool& tools)
     timing.flop = t.flop;
 }
 
+// src/utils.cpp:20-46 (B = A^T for AAT, src/main.cu:98-99) on the device: A must be
+// device-resident; B gets device arrays (and host arrays, as the reference's B).
+inline void matrix_transposition(const CSR& A, CSR& B, Tool& tools) {
+    mhs_csr a{A.M, A.N, A.nnz, A.d_ptr, A.d_col, A.d_val};
+    mhs_csr t{};
+    if (mhs_transpose(tools.ctx, &a, &t) != MHS_OK) throw std::runtime_error(mhs_last_error(tools.ctx));
+    B.release();
+    B.M = t.M;
+    B.N = t.N;
+    B.nnz = t.nnz;
+    B.isSymmetric = 0;
+    B.d_ptr = t.ptr;
+    B.d_col = t.col;
+    B.d_val = t.val;
+    B.D2H();
+}
+
 inline int readMtxFile(CSR& A, const char* filename) {
     mhs_host_csr h{};
     const int rc = mhs_read_mtx(filename, &h);

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 3
+#define MHS_ABI_VERSION 4
 
 typedef enum mhs_status {
     MHS_OK = 0,
@@ -107,6 +107,12 @@ int mhs_ctx_numeric_ms(mhs_ctx *ctx, float *out, int n);
  * Returns after C is complete (the context stream is synchronised), unless
  * MHS_OPT_SYNC is 0.  t may be NULL. */
 int mhs_spgemm(mhs_ctx *ctx, const mhs_csr *A, const mhs_csr *B, mhs_csr *C, mhs_timing *t);
+
+/* At = A^T on the device (the reference's AAT operand: B = transpose(A),
+ * src/main.cu:98-99 with AAT=1, inc/common.h:37; host transpose src/utils.cpp:20-46).
+ * At->M = A->N, At->N = A->M; rows of At list their columns ascending; arrays are
+ * fresh device allocations owned by the caller (mhs_csr_free).  Synchronous. */
+int mhs_transpose(mhs_ctx *ctx, const mhs_csr *A, mhs_csr *At);
 
 /* Free a device CSR produced by mhs_spgemm (hipFree) and zero the struct. */
 void mhs_csr_free(mhs_csr *C);

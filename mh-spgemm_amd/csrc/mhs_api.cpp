@@ -483,6 +483,33 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     return MHS_OK;
 }
 
+int mhs_transpose(mhs_ctx* ctx, const mhs_csr* A, mhs_csr* At) {
+    if (!ctx || !A || !At) return fail(ctx, MHS_ERR_INVALID, "mhs_transpose: null argument");
+    if (A->M < 0 || A->N < 0 || A->nnz < 0 || (A->M > 0 && !A->ptr) || (A->nnz > 0 && (!A->col || !A->val)))
+        return fail(ctx, MHS_ERR_INVALID, "mhs_transpose: malformed A");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail_hip(ctx, e, "hipSetDevice");
+    const Csr a{A->M, A->N, A->nnz, A->ptr, A->col, A->val};
+    size_t tmp_bytes = 0;
+    e = transpose_csr(a, nullptr, nullptr, nullptr, nullptr, &tmp_bytes, ctx->stream);
+    if (e != hipSuccess) return fail_hip(ctx, e, "transpose (scratch size)");
+    mhs_csr T{A->N, A->M, A->nnz, nullptr, nullptr, nullptr};
+    void* tmp = nullptr;
+    e = hipMalloc((void**)&T.ptr, sizeof(int32_t) * ((size_t)A->N + 1));
+    if (e == hipSuccess) e = hipMalloc((void**)&T.col, sizeof(int32_t) * (size_t)(A->nnz ? A->nnz : 1));
+    if (e == hipSuccess) e = hipMalloc((void**)&T.val, sizeof(double) * (size_t)(A->nnz ? A->nnz : 1));
+    if (e == hipSuccess) e = hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16);
+    if (e == hipSuccess) e = transpose_csr(a, T.ptr, T.col, T.val, tmp, &tmp_bytes, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (tmp) (void)hipFree(tmp);
+    if (e != hipSuccess) {
+        mhs_csr_free(&T);
+        return fail_hip(ctx, e, "transpose");
+    }
+    *At = T;
+    return MHS_OK;
+}
+
 int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
     if (!ctx) return MHS_ERR_INVALID;
     switch (option) {

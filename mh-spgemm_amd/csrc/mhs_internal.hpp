@@ -267,6 +267,9 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
                     int* Ccol, double* Cval, hipStream_t s, int global_grid, int dense_span_max);
 size_t sym_global_bytes_per_block(int N);
+// Device CSR transpose (AAT operand): tmp == nullptr -> *tmp_bytes = scratch size.
+hipError_t transpose_csr(const Csr& A, int* tptr, int* tcol, double* tval, void* tmp, size_t* tmp_bytes,
+                         hipStream_t s);
 hipError_t init_kernel_attributes();
 
 }  // namespace mhs

@@ -1,20 +1,33 @@
 // spgemm_main.cpp -- the `spgemm <file.mtx>` driver (reference src/main.cu:74-217)
 // on top of the C-ABI, printing the reference's stdout lines.
 //
-//   spgemm [--iters K] [--warmup W] <file.mtx>
+//   spgemm [--iters K] [--warmup W] [--aat] [--vendor] [--check] [--csv DIR] <file.mtx>
 //
-// Flow as in the reference: read (mmio semantics), reject non-square A (exit 0,
-// main.cu:92-96), B = A, count intermediate products on the host (:102-107),
-// H2D, run MH_spgemm, print per-phase times and GFLOPS = 2*flop/getTotal().
+// Flow as in the reference: read (mmio semantics), reject non-square A unless AAT
+// (exit 0, main.cu:92-96), B = A or B = A^T (AAT and not symmetric, :98-101),
+// count intermediate products on the host (:102-107), H2D, run MH_spgemm, print
+// per-phase times and GFLOPS = 2*flop/getTotal().  The reference's compile-time
+// switches are flags here:
+//   --aat     AAT=1 (inc/common.h:37): C = A * A^T (A^T built on the device)
+//   --vendor  CUSPARSE=1 (inc/common.h:78): the vendor SpGEMM beside it -- rocSPARSE
+//             on this box (include/mhs_vendor.h), its time and GFLOPS (:148-170)
+//   --check   CHECK_RESULT=1: C == vendor C by CSR::operator== -> "pass"/"error" (:186-199)
+//   --csv DIR WRITE=1: append GFLOPS to DIR/Gflops_MH-SpGEMM.csv and, with --vendor,
+//             DIR/Gflops_rocsparse.csv (:173-184, :201-213; the reference's data/)
 // Differences: W untimed warm-up calls (the reference warms the GPU with an
-// empty kernel, MH_spgemm.cuh:10-25), K timed calls averaged (reference iter=1),
-// and an extra e2e line that includes Form_mask_matrix_B.
+// empty kernel, MH_spgemm.cuh:10-25), K timed calls averaged with the context's
+// workspace reused between them (the reference's iter/release loop), and an extra
+// e2e line that includes Form_mask_matrix_B.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
 #include <string>
 
 #include "mh_spgemm.hpp"
+#include "mhs_vendor.h"
 
 static std::string extract_matrix_name(const std::string& path) {
     const size_t s = path.find_last_of("/\\");
@@ -23,57 +36,79 @@ static std::string extract_matrix_name(const std::string& path) {
     return d == std::string::npos ? f : f.substr(0, d);
 }
 
+static bool append_csv(const std::string& dir, const char* file, double gflops) {
+    std::ofstream out(dir + "/" + file, std::ios::app);
+    if (!out) {
+        std::cerr << "Unable to open " << file << std::endl;
+        return false;
+    }
+    out << std::fixed << std::setprecision(2) << gflops << std::endl;
+    return true;
+}
+
+static void recycle(Tool& tools, CSR& C) {
+    mhs_csr c{C.M, C.N, C.nnz, C.d_ptr, C.d_col, C.d_val};
+    mhs_ctx_recycle(tools.ctx, &c);
+    C.d_ptr = C.d_col = nullptr;
+    C.d_val = nullptr;
+}
+
 int main(int argc, char** argv) {
     int iters = 1, warmup = 1;
+    bool aat = false, vendor = false, check = false;
+    std::string csv;
     const char* filename = nullptr;
+    bool bad = false;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--iters") && i + 1 < argc) iters = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--warmup") && i + 1 < argc) warmup = std::atoi(argv[++i]);
-        else if (!filename) filename = argv[i];
-        else filename = nullptr, i = argc;
+        else if (!std::strcmp(argv[i], "--aat")) aat = true;
+        else if (!std::strcmp(argv[i], "--vendor")) vendor = true;
+        else if (!std::strcmp(argv[i], "--check")) check = vendor = true;
+        else if (!std::strcmp(argv[i], "--csv") && i + 1 < argc) csv = argv[++i];
+        else if (!filename && argv[i][0] != '-') filename = argv[i];
+        else bad = true;
     }
-    if (!filename || iters < 1 || warmup < 0) {
+    if (bad || !filename || iters < 1 || warmup < 0) {
         std::puts("Invalid Arguments.");
-        std::puts("Usage:\t ./spgemm [--iters K] [--warmup W] <Input File>");
+        std::puts("Usage:\t ./spgemm [--iters K] [--warmup W] [--aat] [--vendor] [--check] [--csv DIR] <Input File>");
         return -1;
     }
     const std::string matrix_name = extract_matrix_name(filename);
     CSR A, B, C;
     if (readMtxFile(A, filename) != 0) return -1;
-    if (A.M != A.N) {
+    if (!aat && A.M != A.N) {
         std::puts("C=AA must have rowA = colA. Exit.");
         return 0;
     }
     std::printf("--------------------------SpGEMM Start!!!--------------------------\n");
-    B = A;
-    const unsigned long long int_result = mhs_flop_count(A.nnz, A.col, B.ptr);
-    double Gflops = 0;
+    double Gflops = 0, Gflops_v = 0;
+    bool shared_b = false;
     try {
+        Tool tools;
         A.H2D();
-        // B = A: share A's device arrays (C = A*A), no second copy.
-        B.d_ptr = A.d_ptr;
-        B.d_col = A.d_col;
-        B.d_val = A.d_val;
+        if (aat && !A.isSymmetric) {
+            matrix_transposition(A, B, tools);  // device A^T; B's host arrays for the flop count
+        } else {
+            // B = A: share A's device arrays (C = A*A, or A*A^T of a symmetric A), no second copy
+            B = A;
+            B.d_ptr = A.d_ptr;
+            B.d_col = A.d_col;
+            B.d_val = A.d_val;
+            shared_b = true;
+        }
+        const unsigned long long int_result = mhs_flop_count(A.nnz, A.col, B.ptr);
         std::printf("Matrix %s (%d , %d) nnz:%d\n", matrix_name.c_str(), A.M, B.N, A.nnz);
         std::printf("SpGEMM intermediate result = %lld\n", (long long)int_result);
-        Tool tools;
         Timing timing, bench;
         for (int i = 0; i < warmup; ++i) {
             MH_spgemm(A, B, C, timing, tools);
-            mhs_csr c{C.M, C.N, C.nnz, C.d_ptr, C.d_col, C.d_val};
-            mhs_ctx_recycle(tools.ctx, &c);
-            C.d_ptr = C.d_col = nullptr;
-            C.d_val = nullptr;
+            recycle(tools, C);
         }
         for (int i = 0; i < iters; ++i) {
             MH_spgemm(A, B, C, timing, tools);
             bench += timing;
-            if (i < iters - 1) {
-                mhs_csr c{C.M, C.N, C.nnz, C.d_ptr, C.d_col, C.d_val};
-                mhs_ctx_recycle(tools.ctx, &c);
-                C.d_ptr = C.d_col = nullptr;
-                C.d_val = nullptr;
-            }
+            if (i < iters - 1) recycle(tools, C);
         }
         bench /= iters;
         bench.print_step_time();
@@ -81,13 +116,57 @@ int main(int argc, char** argv) {
         std::printf("MH-SpGEMM runtime is %.3lfms, Gflops is %.2lf\n", bench.getTotal(), Gflops);
         std::printf("MH-SpGEMM e2e (incl. form_mask_matrix_B) is %.3lfms, Gflops is %.2lf\n", bench.total_e2e,
                     2.0 * (double)int_result / (bench.total_e2e * 1e6));
+        if (vendor) {
+            mhs_csr a{A.M, A.N, A.nnz, A.d_ptr, A.d_col, A.d_val};
+            mhs_csr b{B.M, B.N, B.nnz, B.d_ptr, B.d_col, B.d_val};
+            mhs_csr v{};
+            double ms = 0;
+            char err[256] = {0};
+            // one untimed call first: rocSPARSE loads its code objects on first use
+            int vrc = mhs_vendor_spgemm(0, &a, &b, &v, &ms, err, (int)sizeof err);
+            if (vrc == MHS_OK) {
+                mhs_vendor_free(&v);
+                vrc = mhs_vendor_spgemm(0, &a, &b, &v, &ms, err, (int)sizeof err);
+            }
+            if (vrc == MHS_OK) {
+                std::printf("rocSPARSE C.nnz = %d\n", v.nnz);
+                Gflops_v = 2.0 * (double)int_result / (ms * 1e6);
+                std::printf("rocsparse: %.3lfms, Gflops is %.2lf\n", ms, Gflops_v);
+                if (check) {
+                    CSR vc;
+                    vc.M = v.M;
+                    vc.N = v.N;
+                    vc.nnz = v.nnz;
+                    vc.d_ptr = v.ptr;
+                    vc.d_col = v.col;
+                    vc.d_val = v.val;
+                    C.D2H();
+                    vc.D2H();
+                    try {
+                        std::puts(C == vc ? "pass" : "error");
+                    } catch (const std::exception&) {
+                        std::puts("error");
+                    }
+                    vc.d_ptr = vc.d_col = nullptr;  // freed below by mhs_vendor_free
+                    vc.d_val = nullptr;
+                }
+                mhs_vendor_free(&v);
+            } else {
+                std::printf("rocSPARSE failed!!! (%s)\n", err);
+            }
+        }
         C.d_release_csr();
-        B.d_ptr = B.d_col = nullptr;
-        B.d_val = nullptr;
     } catch (const std::exception&) {
         std::printf("MH-SpGEMM failed!!!\n");
+        Gflops = 0;
+    }
+    if (shared_b) {  // A owns the device arrays
         B.d_ptr = B.d_col = nullptr;
         B.d_val = nullptr;
+    }
+    if (!csv.empty()) {
+        append_csv(csv, "Gflops_MH-SpGEMM.csv", Gflops);
+        if (vendor) append_csv(csv, "Gflops_rocsparse.csv", Gflops_v);
     }
     std::printf("--------------------------SpGEMM   End!!!--------------------------\n");
     return 0;

@@ -49,9 +49,9 @@ class mhs_host_csr(ctypes.Structure):
                 ("is_symmetric", ctypes.c_int32)]
 
 
-def declared_functions() -> list[str]:
-    """Names of the functions include/mhspgemm.h declares."""
-    text = HEADER.read_text()
+def declared_functions(header: Path | None = None) -> list[str]:
+    """Names of the functions include/mhspgemm.h (or `header`) declares."""
+    text = (header or HEADER).read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(mhs_[a-z0-9_]+)\s*\(", text)))
 
@@ -112,8 +112,34 @@ def lib() -> ctypes.CDLL:
     L.mhs_ctx_numeric_ms.restype = c_int
     L.mhs_device_free.argtypes = [c_void_p, c_void_p]
     L.mhs_device_free.restype = c_int
+    L.mhs_transpose.argtypes = [c_void_p, P(mhs_csr), P(mhs_csr)]
+    L.mhs_transpose.restype = c_int
     _lib = L
     return L
+
+
+VENDOR_PATH = HERE / "libmhs_vendor.so"
+VENDOR_HEADER = HERE.parent.parent / "include" / "mhs_vendor.h"
+_vlib = None
+
+
+def vendor_lib() -> ctypes.CDLL:
+    """libmhs_vendor.so: rocSPARSE SpGEMM, the vendor comparison row (include/mhs_vendor.h)."""
+    global _vlib
+    if _vlib is not None:
+        return _vlib
+    lib()  # torch's HIP runtime first (see lib())
+    if not VENDOR_PATH.exists():
+        raise ImportError(f"{VENDOR_PATH} is missing: build with make -C mh-spgemm_amd")
+    V = ctypes.CDLL(str(VENDOR_PATH))
+    P = ctypes.POINTER
+    V.mhs_vendor_spgemm.argtypes = [ctypes.c_int, P(mhs_csr), P(mhs_csr), P(mhs_csr), P(ctypes.c_double),
+                                    ctypes.c_char_p, ctypes.c_int]
+    V.mhs_vendor_spgemm.restype = ctypes.c_int
+    V.mhs_vendor_free.argtypes = [P(mhs_csr)]
+    V.mhs_vendor_free.restype = None
+    _vlib = V
+    return V
 
 
 def lib_path() -> str:

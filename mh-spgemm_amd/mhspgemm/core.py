@@ -332,6 +332,56 @@ def spgemm(tool: Tool, A: CSR, B: CSR, timing: bool = True):
     return DeviceCSR(tool, c), (Timing.from_c(t) if t is not None else None)
 
 
+def transpose(tool: Tool, A: CSR) -> CSR:
+    """A^T on the device (mhs_transpose): the AAT operand B = transpose(A)
+    (src/main.cu:98-99, host version src/utils.cpp:20-46).  A must be device-
+    resident; the result's device arrays are a library-owned DeviceCSR."""
+    a = A.c_view()
+    t = L.mhs_csr()
+    _check(tool.ctx, L.lib().mhs_transpose(tool.ctx, ctypes.byref(a), ctypes.byref(t)), "mhs_transpose")
+    out = CSR(t.M, t.N)
+    out.nnz = t.nnz
+    out.dev = DeviceCSR(tool, t)
+    return out
+
+
+def matrix_transposition(A: CSR, B: CSR, tool: Tool | None = None) -> None:
+    """src/utils.cpp:20-46 (B = A^T, host arrays) computed on the device: A is
+    uploaded if needed, transposed with mhs_transpose, and B gets host arrays."""
+    own = tool is None
+    tool = tool or Tool(0)
+    try:
+        if A.dev is None and A.d_ptr is None:
+            A.H2D(tool.device)
+        T = transpose(tool, A)
+        B.M, B.N, B.nnz = T.M, T.N, T.nnz
+        B.ptr, B.col, B.val = T.dev.to_host()
+        B.isSymmetric = 0
+        T.d_release_csr()
+    finally:
+        if own:
+            tool.close()
+
+
+def vendor_spgemm(tool: Tool, A: CSR, B: CSR, warmup: int = 0):
+    """rocSPARSE C = A * B (include/mhs_vendor.h; the reference's cusparse_spgemm,
+    inc/cusparse_spgemm.cuh:94-105).  `warmup` untimed calls first (rocSPARSE loads its
+    code objects on first use).  Returns (DeviceCSR, ms over the reference's span)."""
+    V = L.vendor_lib()
+    a, b = A.c_view(), B.c_view()
+    for i in range(warmup + 1):
+        c = L.mhs_csr()
+        ms = ctypes.c_double(0.0)
+        err = ctypes.create_string_buffer(256)
+        rc = V.mhs_vendor_spgemm(tool.device, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                                 ctypes.byref(ms), err, 256)
+        if rc != L.MHS_OK:
+            raise MHSpGEMMError(rc, f"rocSPARSE SpGEMM: {err.value.decode(errors='replace')}")
+        if i < warmup:
+            V.mhs_vendor_free(ctypes.byref(c))
+    return DeviceCSR(tool, c), float(ms.value)
+
+
 def MH_spgemm(A: CSR, B: CSR, C: CSR, timing: Timing, tools: Tool):
     """src/main.cu:12-72: C.M = A.M, C.N = B.N, C.nnz and C's device arrays set;
     phase times written into `timing`.  Raises MHSpGEMMError on failure."""

@@ -289,3 +289,56 @@ def test_cage15_like_rowsample_and_checksum(tool):
     lhs = np.bincount(np.repeat(np.arange(A.M), np.diff(p)), weights=v, minlength=A.M)
     rhs = S @ (S @ ones)
     assert np.allclose(lhs, rhs, rtol=1e-9)
+
+
+# ----------------------------------------------- AAT mode and vendor cross-check ---
+
+@pytest.mark.parametrize("shape", [(700, 1900, 6), (2500, 300, 9), (1, 1, 1)])
+def test_device_transpose_bit_exact(tool, shape):
+    # mhs_transpose vs the oracle's restatement of src/utils.cpp:20-46
+    M, N, per = shape
+    p, c, v = random_csr(M, N, per, seed=M + N)
+    A = mhspgemm.CSR(M, N, p, c, v)
+    A.H2D(tool.device)
+    T = mhspgemm.transpose(tool, A)
+    tp, tc, tv = T.dev.to_host()
+    T.d_release_csr()
+    oM, oN, op, oc, ov = orc.transpose(M, N, p, c, v)
+    assert (T.M, T.N) == (N, M) == (oM, oN)
+    assert np.array_equal(tp, op) and np.array_equal(tc, oc) and np.array_equal(tv, ov)
+
+
+@pytest.mark.parametrize("shape", [(1200, 5000, 7), (3000, 800, 12)])
+def test_aat_rectangular(tool, shape):
+    # AAT=1 (inc/common.h:37, src/main.cu:98-99): C = A * A^T for a non-square A
+    M, N, per = shape
+    p, c, v = random_csr(M, N, per, seed=N)
+    A = mhspgemm.CSR(M, N, p, c, v)
+    A.H2D(tool.device)
+    B = mhspgemm.transpose(tool, A)
+    bp, bc, bv = B.dev.to_host()
+    Bh = mhspgemm.CSR(N, M, bp, bc, bv)
+    t = check(tool, A, Bh)
+    assert t.nnzC > 0
+    B.d_release_csr()
+
+
+@pytest.mark.parametrize("which", ["cage4", "cant", "scircuit", "rect"])
+def test_rocsparse_crosscheck(tool, which):
+    # CUSPARSE + CHECK_RESULT (src/main.cu:148-199): the vendor's C equals ours under
+    # CSR::operator== (pattern exact, values by the reference rule)
+    if which == "rect":
+        p, c, v = random_csr(3000, 2000, 7, 1)
+        Bp, Bc, Bv = random_csr(2000, 50_000, 12, 101)
+        A, B = mhspgemm.CSR(3000, 2000, p, c, v), mhspgemm.CSR(2000, 50_000, Bp, Bc, Bv)
+    else:
+        A = synth.SYNTH[which]()
+        B = A
+    p, c, v, t = run_gpu(tool, A, B)
+    V, ms = mhspgemm.vendor_spgemm(tool, A, B)
+    vp, vc, vv = V.to_host()
+    V.release()
+    assert ms > 0
+    assert np.array_equal(p, vp) and np.array_equal(c, vc)
+    ok, *_ = mhspgemm.compare_tol(vp, vc, vv, p, c, v, RTOL, ATOL)
+    assert ok

@@ -4,6 +4,7 @@ with the golden fixtures and the oracle reader, the reference-mirroring Python
 surface (Timing, CSR ==) behaves like the reference, synthetic generators are
 well-formed.  No compute call reaches the GPU here."""
 import ctypes
+import re
 import subprocess
 from pathlib import Path
 
@@ -27,13 +28,25 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.lib_path()], capture_output=True, text=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert set(names) <= exported
-    assert L.mhs_abi_version() == 3
+    assert L.mhs_abi_version() == 4
+
+
+def test_vendor_library_exports_every_declared_symbol():
+    # rocSPARSE comparison row (include/mhs_vendor.h): loads without a GPU, exports its two entries
+    V = _lib.vendor_lib()
+    names = _lib.declared_functions(_lib.VENDOR_HEADER)
+    assert names == ["mhs_vendor_free", "mhs_vendor_spgemm"]
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.VENDOR_PATH)], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(names) <= exported and all(hasattr(V, n) for n in names)
 
 
 def test_library_is_gfx950_code_object():
     data = Path(_lib.lib_path()).read_bytes()
-    assert b"amdgcn-amd-amdhsa--gfx950" in data
-    assert b"gfx942" not in data and b"gfx90a" not in data  # gfx950 only
+    # every offload-bundle target is gfx950 (rocPRIM's host-side tuning tables name other
+    # architectures as strings; only the code-object targets count)
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx\w+)", data))
+    assert targets == {b"gfx950"}, targets
 
 
 @pytest.mark.parametrize("name", READ_CASES)

@@ -13,6 +13,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("matrices", nargs="*", default=["cant", "webbase-1M", "mac_econ_fwd500", "scircuit", "cop20k_A", "cage15"])
 ap.add_argument("--lib", default=None)
 ap.add_argument("--reps", type=int, default=15)
+ap.add_argument("--vendor", action="store_true", help="also time rocSPARSE (median of 3 after a warm-up)")
 args = ap.parse_args()
 if args.lib:
     os.environ["MHS_LIB"] = str(Path(args.lib).resolve() / "libmhspgemm.so")
@@ -37,6 +38,16 @@ for name in args.matrices:
     out = {"matrix": name, "src": src, "rows": A.M, "nnzA": A.nnz, "flop": int(flop), "nnzC": int(ts[-1].nnzC),
            "gflops_e2e": round(2 * flop / (med["total_e2e"] * 1e-3) / 1e9, 1), **med,
            "sym_bins": list(ts[-1].sym_bins), "num_bins": list(ts[-1].num_bins)}
+    if args.vendor:
+        vms = []
+        for i in range(4):
+            V, ms = mhspgemm.vendor_spgemm(tool, A, A)
+            V.release()
+            if i:
+                vms.append(ms)
+        out["rocsparse_ms"] = round(float(np.median(vms)), 4)
+        out["rocsparse_gflops"] = round(2 * flop / (out["rocsparse_ms"] * 1e-3) / 1e9, 1)
+        out["speedup_vs_rocsparse"] = round(out["rocsparse_ms"] / med["total_e2e"], 2)
     print(json.dumps(out), flush=True)
     A.d_release_csr()
     del A
