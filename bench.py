@@ -11,10 +11,12 @@ allocation included: the t_e2e of BASELINE.md §2), C handed back to the
 context's output pool after the step.
 
 N = 1: one process.  N > 1 (torchrun, one rank per GPU, RCCL): rows of A are
-partitioned by flop, each rank starts with its row block of A (= of B), and a
-step is allgatherv(B) over xGMI + the local SpGEMM; C stays distributed (the
-gathered variant is reported beside it).  Total work is fixed, so scaling is
-"strong".
+partitioned by flop, each rank starts with its row block of A (= of B); the
+exchange plan is built once (mhspgemm.distributed.ShardPlan, outside the timed
+steps) and a step is the exchange of B's rows over xGMI (--exchange halo: the
+rows the block references; full: the north_star's allgatherv of every block)
++ the local SpGEMM; C stays distributed (--gather times the gatherv to rank 0
+beside it).  Total work is fixed, so scaling is "strong".
 
 One JSON line on rank 0: value = 2*flop / (max over ranks of the time per step).
   roofline: the dominant kernel (the numeric phase: k_num_wave for this
@@ -94,6 +96,8 @@ def main():
     ap.add_argument("--matrix", default="cant")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--gather", action="store_true", help="N>1: also time the gatherv of C to rank 0")
+    ap.add_argument("--exchange", default="halo", choices=["halo", "full"],
+                    help="N>1: B rows moved per step: the referenced rows (halo) or every row block (full allgatherv)")
     args = ap.parse_args()
 
     import torch
@@ -164,14 +168,17 @@ def main():
         bnd = D.partition_rows(rf, world)
         blk = D.local_block(A.ptr, A.col, A.val, int(bnd[rank]), int(bnd[rank + 1]), dev)
         mult = D.hip_local_multiply(tool)
+        from mhspgemm import _lib as L
+        tool.set_option(L.MHS_OPT_SYNC, 0)  # stream-ordered calls: no host wait after the numeric launch
+        plan = D.ShardPlan(blk, A.N, mode=args.exchange)  # setup: row plan, buffers (outside the timed steps)
         for _ in range(args.warmup):
-            C, _ = D.spgemm_rowsharded(blk, A.N, mult)
+            C, _ = D.spgemm_planned(plan, mult)
             C.release()
         barrier()
         t0 = time.perf_counter()
         nloc = 0
         for _ in range(args.steps):
-            C, _ = D.spgemm_rowsharded(blk, A.N, mult)
+            C, _ = D.spgemm_planned(plan, mult)
             nloc = C.nnz
             C.release()
         barrier()
@@ -179,11 +186,12 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
-        nn = torch.tensor([nloc], dtype=torch.int64, device=dev)
+        nn = torch.tensor([nloc, plan.bytes_in, plan.nB], dtype=torch.int64, device=dev)
         dist.all_reduce(nn)
-        nnzC = int(nn.item())
+        nnzC, xbytes, xrows = (int(x) for x in nn.tolist())
         if args.gather:
-            C, _ = D.spgemm_rowsharded(blk, A.N, mult)
+            tool.set_option(L.MHS_OPT_SYNC, 1)
+            C, _ = D.spgemm_planned(plan, mult)
             barrier()
             g0 = time.perf_counter()
             D.gather_result(C, blk)
@@ -216,7 +224,8 @@ def main():
         "config": {
             "workload": f"{args.matrix}.mtx A*A ({source}), device-resident A -> device-resident sorted C",
             "matrix": args.matrix, "rows": A.M, "nnzA": A.nnz, "flop": flop, "nnzC": nnzC,
-            "parallelism": "single GPU" if N_GPUS == 1 else f"row-sharded x{N_GPUS}, allgatherv(B) in step, C distributed",
+            "parallelism": "single GPU" if N_GPUS == 1 else
+                           f"row-sharded x{N_GPUS}, {args.exchange} exchange of B's rows in every step, C distributed",
         },
         "e2e_alg_GBps": round(balg / (ms_per_step * 1e-3) / 1e9, 1),
     }
@@ -258,6 +267,8 @@ def main():
     else:
         out["roofline"] = None
         out["cpu_baseline"] = None
+        out["exchange"] = {"mode": args.exchange, "bytes_in_per_step_all_ranks": xbytes,
+                           "local_B_rows_all_ranks": xrows}
         if gather_ms is not None:
             out["gather_C_ms"] = round(gather_ms, 3)
     print(json.dumps(out), flush=True)

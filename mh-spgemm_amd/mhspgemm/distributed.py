@@ -6,12 +6,20 @@ north_star's multi-GPU mode:
 
   1. partition   contiguous A row ranges balanced by flop (products), cut at
                  p*F/P of the int64 prefix sum of per-row flop;
-  2. allgatherv  every rank holds its row block of B (B = A for A*A); the
-                 blocks (row_ptr, col, val) are exchanged with grouped P2P
-                 send/recv straight into place (RCCL has no allgatherv; a
-                 padded all_gather would need a compaction copy) and the
-                 row_ptr blocks rebased by the nnz prefix;
-  3. local       C rows [r_p, r_{p+1}) = A_p * B on each GPU (the HIP library);
+  2. exchange    every rank holds its row block of B (B = A for A*A) and needs
+                 the B rows its A block references.  Two executors of one plan:
+                 * "halo" (default): a rank receives only the rows its columns
+                   name -- the allgatherv restricted to the referenced rows (for
+                   banded / FEM matrices a halo of the neighbours' rows);
+                 * "full": the north_star's allgatherv of every row block.
+                 The plan (which rows go where, receive offsets, A's columns
+                 renumbered to local B rows) is built once by `ShardPlan` with
+                 one all_gather + two all_to_all of counts and row lists; every
+                 step then moves the rows' lengths, columns and values with
+                 grouped P2P send/recv straight into place (RCCL has no
+                 allgatherv) and rebuilds B's row pointer with one cumsum -- no
+                 host round trip inside a step;
+  3. local       C rows [r_p, r_{p+1}) = A_p * B_p on each GPU (the HIP library);
   4. gatherv     optional: C's row blocks to rank 0 (grouped P2P, rebased).
 
 C is left distributed by default -- the gather is reported separately (at 8
@@ -173,7 +181,7 @@ def hip_local_multiply(tool):
     from . import core
 
     def mult(A: Block, Bptr, Bcol, Bval, N):
-        a = core.CSR(A.r1 - A.r0, N)
+        a = core.CSR(A.r1 - A.r0, Bptr.numel() - 1)  # A's columns index the local B rows
         a.nnz = A.col.numel()
         a.d_ptr, a.d_col, a.d_val = A.ptr, A.col, A.val
         b = core.CSR(Bptr.numel() - 1, N)
@@ -203,3 +211,141 @@ def gather_result(C, A_blk: Block, group=None):
     else:
         p, c, v = C.to_torch()
     return gatherv_rows(Block(A_blk.r0, A_blk.r1, p, c, v), 0, group)
+
+
+# ------------------------------------------------------------ planned exchange ---
+
+class ShardPlan:
+    """Inspector/executor exchange of B's rows for a row-sharded A*B (B = A).
+
+    Built once from this rank's block (collectives over `group`); `exchange()`
+    then moves the rows every step.  mode "halo": only the B rows the block's
+    columns reference; "full": every row (the north_star's allgatherv).  The
+    local B keeps rows in ascending global order (owners' ranges are ascending
+    and each request list is sorted), so consecutive rows stay consecutive (FEM
+    dof runs) and A's renumbered columns stay sorted per row."""
+
+    def __init__(self, blk: Block, M_global: int, group=None, mode: str = "halo"):
+        import torch
+        import torch.distributed as dist
+        assert mode in ("halo", "full")
+        self.blk, self.mode, self.group = blk, mode, group
+        P = dist.get_world_size(group)
+        me = dist.get_rank(group)
+        self.P, self.me = P, me
+        dev = blk.col.device
+        self.dev = dev
+        # 1. row ranges of every rank
+        rr = torch.tensor([blk.r0, blk.r1], dtype=torch.int64, device=dev)
+        allr = torch.zeros(2 * P, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allr, rr, group=group)
+        rng = allr.cpu().numpy().reshape(P, 2)
+        self.ranges = rng
+        lptr = blk.ptr.cpu().numpy().astype(np.int64)
+        lcol = blk.col.cpu().numpy()
+        # 2. rows this rank needs from every owner (sorted, global ids)
+        if mode == "full":
+            need = [np.arange(rng[q, 0], rng[q, 1], dtype=np.int64) for q in range(P)]
+        else:
+            u = np.unique(lcol.astype(np.int64))
+            need = [u[(u >= rng[q, 0]) & (u < rng[q, 1])] for q in range(P)]
+        cnt = torch.tensor([len(x) for x in need], dtype=torch.int64, device=dev)
+        cnt_in = torch.zeros(P, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(cnt_in, cnt, group=group)
+        cnt_in = cnt_in.cpu().numpy()
+        req = torch.from_numpy(np.concatenate(need) if P else np.zeros(0, np.int64)).to(dev)
+        req_in = torch.zeros(int(cnt_in.sum()), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(req_in, req, output_split_sizes=cnt_in.tolist(), input_split_sizes=cnt.cpu().tolist(),
+                               group=group)
+        req_in = req_in.cpu().numpy()
+        # 3. what this rank sends: rows (local ids) and their entries, per peer
+        send_rows, send_elems, send_nnz = [], [], []
+        off = 0
+        for q in range(P):
+            rows = req_in[off:off + cnt_in[q]] - blk.r0
+            off += cnt_in[q]
+            send_rows.append(rows)
+            lens = lptr[rows + 1] - lptr[rows]
+            send_nnz.append(int(lens.sum()))
+            send_elems.append(np.repeat(lptr[rows], lens) + (np.arange(lens.sum()) - np.repeat(np.cumsum(lens) - lens, lens)))
+        nnz_out = torch.tensor(send_nnz, dtype=torch.int64, device=dev)
+        nnz_in = torch.zeros(P, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(nnz_in, nnz_out, group=group)
+        nnz_in = nnz_in.cpu().numpy()
+        self.srows = [len(x) for x in send_rows]
+        self.snnz = send_nnz
+        self.rrows = [len(x) for x in need]
+        self.rnnz = [int(x) for x in nnz_in]
+        self.soff_r = np.concatenate([[0], np.cumsum(self.srows)])
+        self.soff_n = np.concatenate([[0], np.cumsum(self.snnz)])
+        self.roff_r = np.concatenate([[0], np.cumsum(self.rrows)])
+        self.roff_n = np.concatenate([[0], np.cumsum(self.rnnz)])
+        cat = lambda xs: np.concatenate(xs) if len(xs) else np.zeros(0, np.int64)  # noqa: E731
+        self.sidx_rows = torch.from_numpy(cat(send_rows).astype(np.int64)).to(dev)
+        self.sidx_elems = torch.from_numpy(cat(send_elems).astype(np.int64)).to(dev)
+        self.rowlen = (blk.ptr[1:] - blk.ptr[:-1]).to(torch.int32)
+        # 4. local B rows (ascending global ids) and A's columns renumbered into them
+        self.brows = cat(need).astype(np.int64)
+        self.nB = len(self.brows)
+        self.Bnnz = int(self.roff_n[-1])
+        pos = np.searchsorted(self.brows, lcol.astype(np.int64))
+        assert len(lcol) == 0 or np.array_equal(self.brows[np.minimum(pos, self.nB - 1)], lcol), "column not planned"
+        self.acol_local = torch.from_numpy(pos.astype(np.int32)).to(dev)
+        self.M_global = M_global
+        # receive buffers (reused every step)
+        self.Blen = torch.empty(self.nB, dtype=torch.int32, device=dev)
+        self.Bcol = torch.empty(self.Bnnz, dtype=blk.col.dtype, device=dev)
+        self.Bval = torch.empty(self.Bnnz, dtype=blk.val.dtype, device=dev)
+        self.Bptr = torch.zeros(self.nB + 1, dtype=torch.int32, device=dev)
+        self.bytes_in = 4 * self.nB + 12 * self.Bnnz - (4 * self.rrows[me] + 12 * self.rnnz[me])
+
+    def exchange(self):
+        """One step: pack the requested rows, P2P them into place, rebuild B's row
+        pointer.  Returns (Bptr, Bcol, Bval) over the local B rows."""
+        import torch
+        import torch.distributed as dist
+        blk, me, P = self.blk, self.me, self.P
+        sl = self.rowlen.index_select(0, self.sidx_rows)
+        sc = blk.col.index_select(0, self.sidx_elems)
+        sv = blk.val.index_select(0, self.sidx_elems)
+        r0, r1 = self.roff_r[me], self.roff_r[me + 1]
+        n0, n1 = self.roff_n[me], self.roff_n[me + 1]
+        s0, s1 = self.soff_r[me], self.soff_r[me + 1]
+        e0, e1 = self.soff_n[me], self.soff_n[me + 1]
+        self.Blen[r0:r1].copy_(sl[s0:s1])
+        self.Bcol[n0:n1].copy_(sc[e0:e1])
+        self.Bval[n0:n1].copy_(sv[e0:e1])
+        ops = []
+        for k in range(1, P):  # ring order spreads the pairs over the xGMI links
+            dst, src = (me + k) % P, (me - k) % P
+            if self.srows[dst]:
+                a, b = self.soff_r[dst], self.soff_r[dst + 1]
+                ops.append(dist.P2POp(dist.isend, sl[a:b], dst, self.group))
+            if self.snnz[dst]:
+                a, b = self.soff_n[dst], self.soff_n[dst + 1]
+                ops.append(dist.P2POp(dist.isend, sc[a:b], dst, self.group))
+                ops.append(dist.P2POp(dist.isend, sv[a:b], dst, self.group))
+            if self.rrows[src]:
+                ops.append(dist.P2POp(dist.irecv, self.Blen[self.roff_r[src]:self.roff_r[src + 1]], src, self.group))
+            if self.rnnz[src]:
+                a, b = self.roff_n[src], self.roff_n[src + 1]
+                ops.append(dist.P2POp(dist.irecv, self.Bcol[a:b], src, self.group))
+                ops.append(dist.P2POp(dist.irecv, self.Bval[a:b], src, self.group))
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+        torch.cumsum(self.Blen, 0, out=self.Bptr[1:])
+        return self.Bptr, self.Bcol, self.Bval
+
+    def local_A(self) -> Block:
+        """This rank's A block with columns renumbered to local B rows."""
+        return Block(self.blk.r0, self.blk.r1, self.blk.ptr, self.acol_local, self.blk.val)
+
+
+def spgemm_planned(plan: ShardPlan, multiply, gather: bool = False):
+    """One row-sharded step with a planned exchange: exchange(B rows), local
+    multiply (A's renumbered columns against the local B), optional gatherv."""
+    Bptr, Bcol, Bval = plan.exchange()
+    C = multiply(plan.local_A(), Bptr, Bcol, Bval, plan.M_global)
+    g = gather_result(C, plan.blk, plan.group) if gather else None
+    return C, g

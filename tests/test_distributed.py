@@ -82,6 +82,80 @@ def _worker(rank, world, port, q):
         q.put({"rank": rank, "error": traceback.format_exc()})
 
 
+def _planned_worker(rank, world, port, q, mode):
+    try:
+        sys.path[:0] = [str(ROOT), str(ROOT / "mh-spgemm_amd"), str(ROOT / "tests")]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world))
+        import torch
+        import torch.distributed as dist
+        from mhspgemm import distributed as D
+        from oracle import oracle as orc
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        M, ptr, col, val = _banded(M=900)
+        rf = D.row_flop(ptr, col, ptr)
+        bnd = D.partition_rows(rf, world)
+        blk = D.local_block(ptr, col, val, int(bnd[rank]), int(bnd[rank + 1]), "cpu")
+        plan = D.ShardPlan(blk, M, mode=mode)
+        # the local B holds exactly the planned rows of the global matrix
+        Bp, Bc, Bv = plan.exchange()
+        rows = plan.brows
+        exp_len = np.diff(ptr)[rows]
+        ok_b = np.array_equal(np.diff(Bp.numpy()), exp_len)
+        sel = np.concatenate([np.arange(ptr[r], ptr[r + 1]) for r in rows]) if len(rows) else np.zeros(0, int)
+        ok_b = ok_b and np.array_equal(Bc.numpy(), col[sel]) and np.array_equal(Bv.numpy(), val[sel])
+        if mode == "halo":  # a banded matrix needs far fewer than all rows on every rank
+            ok_b = ok_b and plan.nB < M
+
+        def mult(A, Bptr, Bcol, Bval, N):
+            Cp, Ci, Cv = orc.spgemm(A.ptr.numpy(), A.col.numpy(), A.val.numpy(), Bptr.numpy(),
+                                    Bcol.numpy(), Bval.numpy(), N)
+            return torch.from_numpy(Cp), torch.from_numpy(Ci), torch.from_numpy(Cv)
+
+        for _ in range(2):  # the plan is reused across steps
+            C, g = D.spgemm_planned(plan, mult, gather=True)
+        res = {"rank": rank, "ok_b": bool(ok_b), "nB": plan.nB}
+        if rank == 0:
+            Cp, Ci, Cv = orc.spgemm(ptr, col, val, ptr, col, val, M)
+            gp, gc, gv = (x.numpy() for x in g)
+            res["ok_c"] = (np.array_equal(gp, Cp) and np.array_equal(gc, Ci) and np.array_equal(gv, Cv))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put(res)
+    except Exception:
+        import traceback
+        q.put({"rank": rank, "error": traceback.format_exc()})
+
+
+def _banded(M=900, width=40, per=8, seed=4):
+    rng = np.random.default_rng(seed)
+    rows = np.repeat(np.arange(M), per)
+    cols = np.clip(rows + rng.integers(-width, width + 1, len(rows)), 0, M - 1)
+    key = np.unique(rows.astype(np.int64) * M + cols)
+    r, c = key // M, (key % M).astype(np.int32)
+    ptr = np.zeros(M + 1, np.int64)
+    np.cumsum(np.bincount(r, minlength=M), out=ptr[1:])
+    return M, ptr.astype(np.int32), c, rng.uniform(0.1, 1.0, len(c))
+
+
+@pytest.mark.parametrize("world,mode", [(2, "halo"), (3, "halo"), (3, "full")])
+def test_planned_exchange_gloo(world, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_planned_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [o["error"] for o in out if "error" in o]
+    assert not errs, errs[0]
+    assert all(o["ok_b"] for o in out), out
+    assert next(o for o in out if o["rank"] == 0)["ok_c"], "gatherv(C) must equal the single-process product"
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_rowsharded_allgatherv_gatherv_gloo(world):
     ctx = mp.get_context("spawn")
