@@ -39,12 +39,8 @@ struct mhs_ctx {
     Published* d_pub = nullptr;
     int seq = 0;
     hipEvent_t ev[8] = {};
-    hipStream_t side = nullptr;  // concurrent block-per-row symbolic bins
-    hipEvent_t fork = nullptr, join = nullptr;
     bool sync = true;      // MHS_OPT_SYNC
     bool groups = true;     // row groups (MHS_NO_GROUPS=1: every row alone)
-    bool use_side = false;  // MHS_SIDE_STREAM=1: block-per-row symbolic bins on a side stream (the
-                            // fork/join costs ~15 us on gfx950: pays only when those bins hold work)
     // MHS_OPT_NUMERIC_EVENTS: ring of (start, end) events around the numeric phase
     std::vector<hipEvent_t> nev;
     long long ncalls = 0;
@@ -71,13 +67,13 @@ int fail_hip(mhs_ctx* ctx, hipError_t e, const char* what) {
 // Spin until the device has published call `seq`'s Stats.  Every 256 polls the
 // stream is queried: a fault ends the wait with the HIP error, an idle stream
 // without the publication is an internal error (never spins forever).
-int wait_published(mhs_ctx* ctx, hipStream_t s, int seq) {
+int wait_published(mhs_ctx* ctx, hipStream_t s, const Published* pub, int seq) {
     for (unsigned polls = 1;; ++polls) {
-        if (__atomic_load_n(&ctx->pub->seq, __ATOMIC_ACQUIRE) == seq) return MHS_OK;
+        if (__atomic_load_n(&pub->seq, __ATOMIC_ACQUIRE) == seq) return MHS_OK;
         if ((polls & 255) == 0) {
             const hipError_t q = hipStreamQuery(s);
             if (q == hipSuccess) {
-                if (__atomic_load_n(&ctx->pub->seq, __ATOMIC_ACQUIRE) == seq) return MHS_OK;
+                if (__atomic_load_n(&pub->seq, __ATOMIC_ACQUIRE) == seq) return MHS_OK;
                 return fail(ctx, MHS_ERR_HIP, "device did not publish the symbolic statistics");
             }
             if (q != hipErrorNotReady) return fail_hip(ctx, q, "waiting for the symbolic phase");
@@ -226,9 +222,6 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (e == hipSuccess) memset(ctx->pub, 0, sizeof(Published));
     for (int i = 0; e == hipSuccess && i < 8; ++i) e = hipEventCreate(&ctx->ev[i]);
     if (e == hipSuccess) e = init_kernel_attributes();
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming);
     if (e != hipSuccess) {
         fprintf(stderr, "mhs_ctx_create: %s\n", hipGetErrorString(e));
         delete ctx;
@@ -237,7 +230,6 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     ctx->stream = ctx->own_stream;
     if (const char* e = getenv("MHS_DENSE_SPAN")) ctx->dense_span_max = atoi(e);
     if (getenv("MHS_NO_MCACHE")) ctx->use_mcache = false;
-    if (const char* e = getenv("MHS_SIDE_STREAM")) ctx->use_side = atoi(e) != 0;
     if (getenv("MHS_NO_GROUPS")) ctx->groups = false;
     *out = ctx;
     return MHS_OK;
@@ -256,12 +248,6 @@ void mhs_ctx_destroy(mhs_ctx* ctx) {
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
-    if (ctx->side) {
-        (void)hipStreamSynchronize(ctx->side);
-        (void)hipStreamDestroy(ctx->side);
-    }
-    if (ctx->fork) (void)hipEventDestroy(ctx->fork);
-    if (ctx->join) (void)hipEventDestroy(ctx->join);
     delete ctx;
 }
 
@@ -376,8 +362,10 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     launch_analyze(a, w, MB, s, out.ptr);
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[2], s));
     // ---- Calculate_C_nnz ------------------------------------------------------------
-    MHS_HIP(launch_symbolic(a, b, w, M, N, out.ptr, s, sym_grid, ctx->use_side ? ctx->side : nullptr, ctx->fork,
-                            ctx->join));
+    // persistent grids that read their bins' sizes on the device: no host round trip
+    launch_symbolic_common(a, b, w, M, N, out.ptr, s);
+    launch_symbolic_rare(a, w, M, N, out.ptr, s, sym_grid);
+    MHS_HIP(hipGetLastError());
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
     Stats h;
@@ -388,7 +376,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
         MHS_HIP(hipGetLastError());
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
-        rc = wait_published(ctx, s, seq);
+        rc = wait_published(ctx, s, ctx->pub, seq);
         if (rc) {
             pool_put(ctx, out.ptr);
             return rc;

@@ -26,6 +26,7 @@ constexpr int TILE_SHIFT = 6;  // 64-column tiles, one uint64 mask each (wave64 
 constexpr int TILE_BITS = 64;
 constexpr int NBINS = 16;  // capacity of the per-bin counters
 constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
+constexpr int LDS_MAX_C = 163840;  // gfx950: 160 KiB per workgroup (probed on the box)
 constexpr int SCAN_ITEMS = 1024;// rows per block in the row_ptr scan and the bin-list passes
 
 // Symbolic bins (by LDS need and tile work).
@@ -75,7 +76,7 @@ constexpr int GRP_CONT = 0x80;
 // Per-team LDS budgets (bytes).  The wave kernels carve one region per wave.
 constexpr int SYM_WAVE_BYTES = 5120;   // 4 waves x 5 KiB: 8 blocks (32 waves, the CU's cap) per CU
 constexpr int SYM_WAVE_WORK = 4096;     // tile products a single wave takes on
-constexpr int SYM_WM_BYTES = 10240;   // 4 waves x 10 KiB: 4 blocks (16 waves) per CU
+constexpr int SYM_WM_BYTES = (LDS_MAX_C - 1024) / 16;  // 16 waves of a 1024-thread block (k_sym_rare): 16 waves per CU
 constexpr int SYM_B256_BYTES = 32768;
 constexpr int SYM_B256_WORK = 1 << 20;
 constexpr int NUM_WS_BYTES = 5120;   // 4 waves x 5 KiB = 20 KiB/block: 8 blocks (32 waves) per CU
@@ -259,9 +260,8 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);
 void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr);
 int analyze_blocks(long long nnzA, int M);
 
-hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s,
-                           int global_grid, hipStream_t side = nullptr, hipEvent_t fork = nullptr,
-                           hipEvent_t join = nullptr);
+void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s);
+void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid);
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
                           Published* pub, int seq);
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,

@@ -27,6 +27,7 @@
 // neighbouring rows (which share B rows) run on one XCD's L2.
 #include "mhs_internal.hpp"
 
+#include <algorithm>
 #include <climits>
 
 #ifndef MHS_NUM_DIAG
@@ -522,6 +523,22 @@ __device__ __forceinline__ int sym_bin_of(int flop, int tflop, int span) {
     if (need <= SYM_B256_BYTES - BLOCK_HDR && tflop <= SYM_B256_WORK) return SYM_B256;
     if (need <= B1024_BYTES) return SYM_B1024;
     return SYM_GLOBAL;
+}
+
+// Stats -> fine-grained pinned host memory, then the sequence number the host spins
+// on (one block: L1-bypassing reads, system-scope stores, release of the number).
+__device__ void publish_stats(const Stats* stats, Published* pub, int seq) {
+    constexpr int NW = (int)(sizeof(Stats) / 4);
+    static_assert(sizeof(Stats) % 4 == 0 && NW <= 1024, "Stats is copied one word per thread");
+    const int* src = reinterpret_cast<const int*>(stats);
+    int* dst = reinterpret_cast<int*>(&pub->stats);
+    if (threadIdx.x < NW)
+        __hip_atomic_store(dst + threadIdx.x,
+                           __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Last block of a grid to reach this point (after its writes): returns true in
@@ -1337,6 +1354,42 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
 }
 
+// Every rare symbolic bin in one launch (their sizes are on the device; an empty bin
+// costs nothing but its loop test): 1024-thread blocks holding all 160 KiB of LDS.
+//   phase 0  global-memory rows (blocks < gg, tables in global scratch),
+//   phase 1  rows for the 1024-thread block's LDS table,
+//   phase 2  rows for a 10 KiB table: a wave per row, 16 waves per block.
+// (Rows for a 32 KiB table keep a 256-thread kernel of their own: at one block per CU
+// they would have a fifth of the rows in flight.)
+__global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a, int gg) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int4* stage = (int4*)(smem + 1024);
+    if ((int)blockIdx.x < gg) {
+        BlockTeam<1024, true> tg{(long long*)smem};
+        TileEntry* E = (TileEntry*)(a.gscratch + (long long)blockIdx.x * a.gbytes);
+        const int count = a.stats->sym_count[SYM_GLOBAL];
+        const int* list = a.list + (long long)(SYM_GLOBAL - 1) * a.M;
+        for (RowWalk rw(count, 1, 0, (int)blockIdx.x, gg); rw.first < rw.end; rw.first += rw.stride)
+            sym_row(tg, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
+    }
+    BlockTeam<1024, false> tm{(long long*)smem};
+    TileEntry* E = (TileEntry*)(smem + BLOCK_HDR);
+    {
+        const int count = a.stats->sym_count[SYM_B1024];
+        const int* list = a.list + (long long)(SYM_B1024 - 1) * a.M;
+        for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
+            sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
+    }
+    __syncthreads();  // phase 2 reuses the whole LDS
+    const int w = threadIdx.x >> 6;
+    TileEntry* Ew = (TileEntry*)(smem + w * SYM_WM_BYTES + WAVE_HDR);
+    const int count = a.stats->sym_count[SYM_WM];
+    const int* list = a.list + (long long)(SYM_WM - 1) * a.M;
+    WaveTeam wt;
+    for (RowWalk rw(count, 16, w); rw.first < rw.end; rw.first += rw.stride)
+        sym_row(wt, a, __builtin_amdgcn_readfirstlane(list[rw.first]), Ew, nullptr);
+}
+
 // ----------------------------------------------------- scan + classify ---
 
 // Append a 1024-thread block's SCAN_ITEMS rows (blockIdx*SCAN_ITEMS + j, bins in
@@ -1561,19 +1614,7 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
     __syncthreads();
     append_block_rows<NUM_NB>(nbin_of, M, stats->num_count, list);
     if (!last_block_done(&stats->final_done)) return;
-    if (pub) {  // L1-bypassing reads, system-scope stores, release of the sequence number
-        constexpr int NW = (int)(sizeof(Stats) / 4);
-        static_assert(sizeof(Stats) % 4 == 0 && NW <= 1024, "Stats is copied one word per thread");
-        const int* src = reinterpret_cast<const int*>(stats);
-        int* dst = reinterpret_cast<int*>(&pub->stats);
-        if (threadIdx.x < NW)
-            __hip_atomic_store(dst + threadIdx.x,
-                               __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (pub) publish_stats(stats, pub, seq);
 }
 
 // --------------------------------------------------------------- numeric ---
@@ -2184,6 +2225,8 @@ hipError_t init_kernel_attributes() {
     hipError_t e = hipFuncSetAttribute((const void*)k_sym_block<1024, false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_sym_rare, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_num_block<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 LDS_MAX);
     if (e == hipSuccess)
@@ -2222,9 +2265,7 @@ static void launch_tiny_num(int c, int rows, const TinyArgs& t, hipStream_t s) {
 #undef MHS_TINY
 }
 
-hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s,
-                           int global_grid, hipStream_t side, hipEvent_t fork, hipEvent_t join) {
-    if (M <= 0) return hipSuccess;
+static SymArgs sym_args(const Csr& A, const Work& w, int M, int N, int* Cptr) {
     SymArgs a;
     a.M = M;
     a.Aptr = A.ptr;
@@ -2243,49 +2284,41 @@ hipError_t launch_symbolic(const Csr& A, const Csr& B, const Work& w, int M, int
     a.gscratch = (char*)w.gscratch;
     a.gbytes = (long long)sym_global_bytes_per_block(N);
     a.mcache = w.mcache;
-    // Persistent grids: the bin sizes stay on the device (no host round trip);
-    // blocks past a bin's rows exit at once.  The block-per-row bins run on the side
-    // stream, concurrently with the wave bin (rows are independent): their launches,
-    // empty or not, overlap the wave kernel instead of following it.
-    hipStream_t sb = s;
-    if (side) {
-        hipError_t e = hipEventRecord(fork, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
-        if (e != hipSuccess) return e;
-        sb = side;
-    }
-    a.bin = SYM_GLOBAL;
-    hipLaunchKernelGGL((k_sym_block<1024, true>), dim3(global_grid), dim3(1024), BLOCK_HDR, sb, a);
-    a.bin = SYM_B1024;
-    hipLaunchKernelGGL((k_sym_block<1024, false>), dim3(round8(M, 256)), dim3(1024), LDS_MAX - 1024, sb, a);
-    a.bin = SYM_B256;
-    hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, 1024)), dim3(256), SYM_B256_BYTES, sb, a);
+    a.bin = 0;
+    return a;
+}
+
+// The common symbolic bins, launched right after the row analysis with persistent
+// grids that read their bin's size on the device: the small-table wave bin and
+// every tiny class (one launch).
+void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s) {
+    if (M <= 0) return;
+    SymArgs a = sym_args(A, w, M, N, Cptr);
     a.bin = SYM_WAVE;
     hipLaunchKernelGGL(k_sym_wave<SYM_WAVE_BYTES>, dim3(round8((M + WPB - 1) / WPB, 2048)), dim3(256),
                        WPB * SYM_WAVE_BYTES, s, a);
-    a.bin = SYM_WM;
-    hipLaunchKernelGGL(k_sym_wave<SYM_WM_BYTES>, dim3(round8((M + WPB - 1) / WPB, 1024)), dim3(256),
-                       WPB * SYM_WM_BYTES, s, a);
-    {
-        TinyArgs t{};
-        t.M = M;
-        t.Aptr = A.ptr;
-        t.Acol = A.col;
-        t.bmeta = w.bmeta;
-        t.Bcol = B.col;
-        t.stats = w.stats;
-        t.grp = w.grp;
-        t.Cptr = Cptr;
-        t.ctiles = w.ctiles;
-        t.list = w.bin_list + (long long)(SYM_TINY - 1) * M;
-        hipLaunchKernelGGL(k_tiny_sym, dim3(TINY_SYM_GRID * TINY_SYM_NC), dim3(256), 0, s, t);
-    }
-    if (side) {
-        hipError_t e = hipEventRecord(join, side);
-        if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
-        return e;
-    }
-    return hipSuccess;
+    TinyArgs t{};
+    t.M = M;
+    t.Aptr = A.ptr;
+    t.Acol = A.col;
+    t.bmeta = w.bmeta;
+    t.Bcol = B.col;
+    t.stats = w.stats;
+    t.grp = w.grp;
+    t.Cptr = Cptr;
+    t.ctiles = w.ctiles;
+    t.list = w.bin_list + (long long)(SYM_TINY - 1) * M;
+    hipLaunchKernelGGL(k_tiny_sym, dim3(TINY_SYM_GRID * TINY_SYM_NC), dim3(256), 0, s, t);
+}
+
+// The rare bins (10 KiB waves, 32 KiB and 157 KiB block tables, global memory): one
+// persistent launch that reads the bins' sizes on the device.
+void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid) {
+    if (M <= 0) return;
+    SymArgs a = sym_args(A, w, M, N, Cptr);
+    hipLaunchKernelGGL(k_sym_rare, dim3(std::max(256, global_grid)), dim3(1024), LDS_MAX - 1024, s, a, global_grid);
+    a.bin = SYM_B256;
+    hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, 1024)), dim3(256), SYM_B256_BYTES, s, a);
 }
 
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
