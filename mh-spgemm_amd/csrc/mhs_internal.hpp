@@ -105,7 +105,7 @@ struct Stats {
     unsigned long long flop;       // total products
     long long nnzC;                // total C nnz (scan result)
     int err;                       // error bits (ERR_*)
-    int scan_done;                 // k_scan_reduce blocks finished (last one scans the partials)
+    int scan_ticket;               // k_scan's dynamic block index (look-back order = dispatch order)
     int sym_count[NBINS];
     int num_count[NBINS];
     int num_global_need;           // max LDS-equivalent bytes of a global numeric row
@@ -249,7 +249,7 @@ struct Work {
     int* bin_list;           // (NUM_NB-1) * M: bin x's rows at (x-1)*M (symbolic bins, then numeric bins)
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count
-    int* scan_part;    // block sums of the row_ptr scan (long long stored as 2 ints)
+    int* scan_part;    // k_scan's look-back state: one 64-bit word per block (flag | prefix)
     unsigned long long* mcache;   // [M][MCACHE_SPAN] tile masks of narrow rows (symbolic -> numeric)
     Stats* stats;
     void* gscratch;    // global-bin scratch

@@ -632,10 +632,13 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
                                                  unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
                                                  unsigned long long* __restrict__ blkflop,
                                                  unsigned char* __restrict__ asame,
-                                                 Stats* __restrict__ stats) {
+                                                 Stats* __restrict__ stats,
+                                                 unsigned long long* __restrict__ lb_state, int nlb) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nlb; i += gridDim.x * blockDim.x)
+        lb_state[i] = 0ull;  // k_scan's look-back words (k_scan runs after every analyze block)
     const bool valid = row < M;
     int err = 0;
     bool lng = false;
@@ -1398,7 +1401,7 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a, int gg) {
 // their places (the grids that call this have M/4096 blocks: little contention).
 template <int NB>
 __device__ void append_block_rows(const unsigned char* binof, long long M, int* __restrict__ cnt,
-                                  int* __restrict__ list) {
+                                  int* __restrict__ list, int blk) {
     constexpr int PER = SCAN_ITEMS / 1024;
     static_assert(PER * 16 <= 64 && NB <= 16, "one wave scans one bin's (pass, wave) counts");
     __shared__ int wc[NB][PER * 16];  // [bin][pass*16 + wave]: members, then exclusive prefix
@@ -1428,7 +1431,7 @@ __device__ void append_block_rows(const unsigned char* binof, long long M, int* 
         const int x = mybin[k];
         if (x > 0)
             list[(long long)(x - 1) * M + nbase[x] + wc[x][k * 16 + w] + rank[k]] =
-                blockIdx.x * SCAN_ITEMS + k * 1024 + threadIdx.x;
+                blk * SCAN_ITEMS + k * 1024 + threadIdx.x;
     }
 }
 
@@ -1463,48 +1466,7 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
         binof[j] = b;
     }
     __syncthreads();
-    append_block_rows<SYM_NB>(binof, M, cnt, list);
-}
-
-// Exclusive scan of the per-block partials (one block; run by the last reduce block).
-__device__ void scan_partials(int nb, long long* __restrict__ part, Stats* __restrict__ stats,
-                              const unsigned long long* __restrict__ blkflop, int nflop) {
-    {  // total products = sum of k_analyze's per-block partials
-        __shared__ unsigned long long fs[16];
-        unsigned long long f = 0;
-        for (int i = threadIdx.x; i < nflop; i += 1024) f += blkflop[i];
-        f = wave_sum(f);
-        if (lane_id() == 0) fs[threadIdx.x >> 6] = f;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long t = 0;
-            for (int k = 0; k < 16; ++k) t += fs[k];
-            stats->flop = t;
-        }
-    }
-    __shared__ long long ws[16];
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    long long carry = 0;
-    for (int b = 0; b < nb; b += 1024) {
-        const int i = b + threadIdx.x;
-        const long long x = i < nb ? __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        const long long inc = wave_incl_scan64(x);
-        if (lane == 63) ws[w] = inc;
-        __syncthreads();
-        long long woff = 0, tot = 0;
-        for (int k = 0; k < 16; ++k) {
-            const long long v = ws[k];
-            woff += (k < w) ? v : 0;
-            tot += v;
-        }
-        if (i < nb) part[i] = carry + woff + inc - x;
-        carry += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        stats->nnzC = carry;
-        if (carry > INT_MAX) atomicOr(&stats->err, ERR_OVERFLOW);
-    }
+    append_block_rows<SYM_NB>(binof, M, cnt, list, (int)blockIdx.x);
 }
 
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
@@ -1535,43 +1497,35 @@ __device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t
     return NUM_NONE;
 }
 
-// Exclusive scan of the C row nnz (items [0, M], item M = 0 gives row_ptr[M])
-// plus the numeric bin of every row.
-__global__ __launch_bounds__(1024) void k_scan_reduce(int M, const int* __restrict__ Cptr,
-                                                      long long* __restrict__ part, Stats* __restrict__ stats,
-                                                      const unsigned long long* __restrict__ blkflop, int nflop) {
+// Row pointer = exclusive scan of the C row nnz (items [0, M]; item M = 0 gives
+// row_ptr[M]) in ONE pass with decoupled look-back: blocks take tickets in dispatch
+// order, publish their aggregate, add up their predecessors' (inclusive prefix once
+// one is found) and publish their own inclusive prefix.  Every predecessor holds an
+// earlier ticket, so it has started and publishes without waiting on this block.  The
+// same pass gives every row its numeric bin and appends it to the bin lists; the last
+// block to finish totals the products and publishes Stats to the host.
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+__global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
+                                               unsigned long long* __restrict__ state,
+                                               const int* __restrict__ rflop,
+                                               const int* __restrict__ rlo,
+                                               const int* __restrict__ rhi,
+                                               const int* __restrict__ ctiles,
+                                               const unsigned char* __restrict__ grp,
+                                               const int* __restrict__ Aptr,
+                                               int* __restrict__ list, Stats* __restrict__ stats,
+                                               int dense_span_max, Published* pub, int seq, int tiny_ok,
+                                               const unsigned long long* __restrict__ blkflop, int nflop) {
+    static_assert(SCAN_ITEMS == 1024, "one item per thread");
+    constexpr int PER = 1;
     __shared__ long long ws[16];
-    const int base = blockIdx.x * SCAN_ITEMS;
-    long long s = 0;
-    for (int k = threadIdx.x; k < SCAN_ITEMS; k += 1024) {
-        const int i = base + k;
-        if (i < M) s += Cptr[i];
-    }
-    s = wave_sum(s);
-    if (lane_id() == 0) ws[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        long long t = 0;
-        for (int k = 0; k < 16; ++k) t += ws[k];
-        part[blockIdx.x] = t;
-    }
-    if (last_block_done(&stats->scan_done)) scan_partials(gridDim.x, part, stats, blkflop, nflop);
-}
-
-__global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cptr,
-                                                     const long long* __restrict__ part,
-                                                     const int* __restrict__ rflop,
-                                                     const int* __restrict__ rlo,
-                                                     const int* __restrict__ rhi,
-                                                     const int* __restrict__ ctiles,
-                                                     const unsigned char* __restrict__ grp,
-                                                     const int* __restrict__ Aptr,
-                                                     int* __restrict__ list, Stats* __restrict__ stats,
-                                                     int dense_span_max, Published* pub, int seq, int tiny_ok) {
-    constexpr int PER = SCAN_ITEMS / 1024;
-    __shared__ long long ws[16];
+    __shared__ long long excl_s;
+    __shared__ int bid_s;
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const int base = blockIdx.x * SCAN_ITEMS + threadIdx.x * PER;
+    if (threadIdx.x == 0) bid_s = atomicAdd(&stats->scan_ticket, 1);
+    __syncthreads();
+    const int bid = bid_s;
+    const int base = bid * SCAN_ITEMS + threadIdx.x * PER;
     int v[PER];
     long long loc = 0;
 #pragma unroll
@@ -1583,9 +1537,37 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
     const long long inc = wave_incl_scan64(loc);
     if (lane == 63) ws[w] = inc;
     __syncthreads();
-    long long off = part[blockIdx.x];
-    for (int k = 0; k < w; ++k) off += ws[k];
-    off += inc - loc;
+    long long woff = 0, total = 0;
+    for (int k = 0; k < 16; ++k) {
+        woff += k < w ? ws[k] : 0;
+        total += ws[k];
+    }
+    if (threadIdx.x == 0) {
+        long long ex = 0;
+        if (bid > 0) {
+            __hip_atomic_store(&state[bid], LB_AGG | (unsigned long long)total, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            for (int j = bid - 1;;) {
+                const unsigned long long st = __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (st == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;  // predecessor running: its aggregate comes without waiting on us
+                }
+                ex += (long long)(st & LB_VAL);
+                if (st & LB_INC) break;
+                --j;
+            }
+        }
+        __hip_atomic_store(&state[bid], LB_INC | (unsigned long long)(ex + total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        excl_s = ex;
+        if (bid == (int)gridDim.x - 1) {
+            stats->nnzC = ex + total;
+            if (ex + total > INT_MAX) atomicOr(&stats->err, ERR_OVERFLOW);
+        }
+    }
+    __syncthreads();
+    long long off = excl_s + woff + inc - loc;
     __shared__ unsigned char nbin_of[SCAN_ITEMS];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -1612,8 +1594,22 @@ __global__ __launch_bounds__(1024) void k_scan_final(int M, int* __restrict__ Cp
         off += v[k];
     }
     __syncthreads();
-    append_block_rows<NUM_NB>(nbin_of, M, stats->num_count, list);
+    append_block_rows<NUM_NB>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
+    {  // total products = sum of k_analyze's per-block partials
+        __shared__ unsigned long long fs[16];
+        unsigned long long f = 0;
+        for (int i = threadIdx.x; i < nflop; i += 1024) f += blkflop[i];
+        f = wave_sum(f);
+        if (lane == 0) fs[w] = f;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long t = 0;
+            for (int k = 0; k < 16; ++k) t += fs[k];
+            stats->flop = t;
+        }
+        __syncthreads();
+    }
     if (pub) publish_stats(stats, pub, seq);
 }
 
@@ -2207,7 +2203,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats)
+#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS)
     switch (G) {
     case 8: MHS_ANALYZE(8); break;
     case 16: MHS_ANALYZE(16); break;
@@ -2323,11 +2319,10 @@ void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, 
 
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
                           Published* pub, int seq) {
-    const int nb = (M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS;
-    long long* part = (long long*)w.scan_part;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.stats, w.blkflop, w.nflop);
-    hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(1024), 0, s, M, Cptr, part, w.rflop, w.rlo, w.rhi,
-                       w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num);
+    const int nb = (M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS;  // the state words were zeroed by k_analyze
+    hipLaunchKernelGGL(k_scan, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop, w.rlo,
+                       w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num,
+                       w.blkflop, w.nflop);
 }
 
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
