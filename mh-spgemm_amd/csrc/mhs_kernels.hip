@@ -1661,7 +1661,10 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     // 1. the C row's tile table: the symbolic pass's masks when it kept them,
     //    else rebuilt (same OR pass as symbolic)
     MHS_STAMP(0);
-    if (MODE != NM_HASH && a.mcache && mcached(span, tflop)) {
+    // symbolic kept the masks unless it sorted the row as a tiny one (numeric runs those
+    // with tables when the tiny classes are off: N beyond the packed keys' 23 bits)
+    const bool sym_tiny = tiny_class(__builtin_amdgcn_readfirstlane(a.rflop[row]), a1 - a0, TINY_SYM_NC) >= 0;
+    if (MODE != NM_HASH && a.mcache && mcached(span, tflop) && !sym_tiny) {
         for (int s = tm.rank(); s < span; s += Team::size) {
             TileEntry z;
             z.mask = a.mcache[(size_t)row * MCACHE_SPAN + s];

@@ -342,3 +342,19 @@ def test_rocsparse_crosscheck(tool, which):
     assert np.array_equal(p, vp) and np.array_equal(c, vc)
     ok, *_ = mhspgemm.compare_tol(vp, vc, vv, p, c, v, RTOL, ATOL)
     assert ok
+
+
+def test_wide_column_space_small_rows(tool):
+    # N > 2^23: the numeric tiny classes are off (packed sort keys hold 23 column bits),
+    # so rows the symbolic phase sorted (tiny) run the table kernels in numeric, with
+    # narrow spans that would qualify for cached tile masks symbolic never wrote
+    rng = np.random.default_rng(12)
+    N = 9_000_000
+    p, c, v = random_csr(3000, 400, 4, seed=12)
+    A = mhspgemm.CSR(3000, 400, p, c, v)
+    Bp, Bc, Bv = random_csr(400, 1500, 6, seed=13)
+    Bc = (Bc + 8_600_000).astype(np.int32)  # every column past 2^23, within ~24 tiles
+    B = mhspgemm.CSR(400, N, Bp, Bc, Bv)
+    t = check(tool, A, B)
+    assert t.sym_bins[5] + t.sym_bins[6] > 0, t.sym_bins
+    assert all(t.num_bins[i] == 0 for i in range(8, 14)), t.num_bins

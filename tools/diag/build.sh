@@ -11,7 +11,8 @@ for v in "$@"; do
 done
 wait
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -x hip -c $SRC/mhs_api.cpp -o api.o
+[ tr.o -nt $SRC/mhs_transpose.hip ] || hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c $SRC/mhs_transpose.hip -o tr.o
 hipcc -O3 -std=c++17 -fPIC -c $SRC/mhs_mmio.cpp -o mmio.o
 for v in "$@"; do
-  hipcc --offload-arch=gfx950 -shared -fPIC -o v$v/libmhspgemm.so v$v/k.o api.o mmio.o -lpthread
+  hipcc --offload-arch=gfx950 -shared -fPIC -o v$v/libmhspgemm.so v$v/k.o tr.o api.o mmio.o -lpthread
 done
