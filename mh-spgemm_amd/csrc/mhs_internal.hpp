@@ -185,6 +185,11 @@ __host__ __device__ inline long long num_need_rmap(int span, int n) {
 }
 // symbolic stores the OR'd tile masks of rows it tabled direct-mapped over a narrow span
 __host__ __device__ inline bool mcached(int span, int tflop) { return span <= MCACHE_SPAN && sym_direct(span, tflop); }
+// ... and of the other rows with at most MC_LIST distinct tiles, a compact list in the same
+// 256-byte slot: masks at [0, 16), tile keys (int32) in the next 64 bytes
+constexpr int MC_LIST = 16;
+static_assert(MC_LIST * 12 <= MCACHE_SPAN * 8, "the tile list fits the row's cache slot");
+__host__ __device__ inline bool mlisted(int span, int tflop, int t) { return !mcached(span, tflop) && t <= MC_LIST; }
 __host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_max) {
     if (span <= dense_span_max) return NM_DENSE;
     if (span <= RMAP_SPAN_MAX) return NM_RMAP;

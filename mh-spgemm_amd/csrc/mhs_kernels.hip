@@ -78,6 +78,21 @@
 #ifndef MHS_BLOCKDIST
 #define MHS_BLOCKDIST 1  // A entries -> lane groups: 1 block distribution, 0 cyclic
 #endif
+// Occupancy targets (waves per SIMD; 0 = the compiler's choice).  The wave kernels are
+// bound by per-row latency chains, so waves in flight matter more than a few spills.
+#ifndef MHS_WPE_HASH
+#define MHS_WPE_HASH 8  // measured: cop20k-like numeric -18%, cage15-like -16% (vs the compiler's 6)
+#endif
+#ifndef MHS_WPE_DIRECT
+#define MHS_WPE_DIRECT 0
+#endif
+#ifndef MHS_WPE_TINY
+#define MHS_WPE_TINY 0
+#endif
+#define MHS_WPE_ATTR(n) __attribute__((amdgpu_waves_per_eu((n) > 0 ? (n) : 1)))
+#ifndef MHS_WPE_SYM
+#define MHS_WPE_SYM 8  // symbolic wave + tiny kernels: cant-like -12%, cop20k-like -22%
+#endif
 #if MHS_NUM_DIAG == 9  // diagnostic build: per-row, per-phase s_memtime cycles (plain stores)
 __device__ unsigned long long* g_rowdiag;  // [M][8]
 #define MHS_STAMP0() unsigned long long tp_ = __builtin_amdgcn_s_memtime()
@@ -1329,11 +1344,33 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
         const unsigned long long m = E[r_].mask;
         for (int g = 0; g < R; ++g) a.mcache[(size_t)(row + g) * MCACHE_SPAN + r_] = m;
     }
+    // ... and the compacted (key, mask) list of the other rows with few tiles
+    if (a.mcache && mlisted(span, tflop, t) && r_ < 64) {  // the first wave compacts the table
+        const int lane = lane_id();
+        int k = 0;
+        for (int s0 = 0; s0 < H; s0 += 64) {
+            const int sl = s0 + lane;
+            uint4 q = make_uint4(0, 0, 0, 0);
+            if (sl < H) q = *reinterpret_cast<const uint4*>(&E[sl]);  // mask, base, key
+            const bool occ = (q.x | q.y) != 0u;
+            const unsigned long long bal = __ballot(occ);
+            if (occ) {
+                const int pos = k + __popcll(bal & lanemask_lt());
+                const int key = direct ? lo + sl : (int)q.w;
+                for (int g = 0; g < R; ++g) {
+                    unsigned long long* slot = a.mcache + (size_t)(row + g) * MCACHE_SPAN;
+                    slot[pos] = ((unsigned long long)q.y << 32) | q.x;
+                    reinterpret_cast<int*>(slot + MC_LIST)[pos] = key;
+                }
+            }
+            k += __popcll(bal);
+        }
+    }
     tm.sync();
 }
 
 template <int BYTES>
-__global__ __launch_bounds__(256) void k_sym_wave(SymArgs a) {
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_wave(SymArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int w = threadIdx.x >> 6;
     TileEntry* E = (TileEntry*)(smem + w * BYTES + WAVE_HDR);
@@ -1673,6 +1710,25 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             E[s] = z;
         }
         tm.sync();
+    } else if (a.mcache && mlisted(span, tflop, t) && !sym_tiny) {
+        // symbolic's compacted list: t <= 16 (key, mask) pairs, one per lane
+        clear_tiles(tm, E, H);
+        if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
+        tm.sync();
+        const int r = tm.rank();
+        if (r < t) {
+            const unsigned long long* slot = a.mcache + (size_t)row * MCACHE_SPAN;
+            const unsigned long long m = slot[r];
+            const int key = reinterpret_cast<const int*>(slot + MC_LIST)[r];
+            if (MODE != NM_HASH) {
+                E[key - lo].mask = m;
+            } else {
+                int sl = hslot(key, hshift);
+                while (atomicCAS(&E[sl].key, -1, key) != -1) sl = (sl + 1) & (H - 1);  // keys are distinct
+                E[sl].mask = m;
+            }
+        }
+        tm.sync();
     } else {
         clear_tiles(tm, E, H);
         if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
@@ -1923,8 +1979,9 @@ __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region,
         num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
 }
 
-template <int BYTES, bool GROUPED = false, bool HASH = false>
-__global__ __launch_bounds__(256, MHS_NUM_WAVES_EU) void k_num_wave(NumArgs a) {
+
+template <int BYTES, bool GROUPED, bool HASH>
+__device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int w = threadIdx.x >> 6;
     char* reg = smem + w * BYTES;
@@ -1938,6 +1995,19 @@ __global__ __launch_bounds__(256, MHS_NUM_WAVES_EU) void k_num_wave(NumArgs a) {
             num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH>(tm, a, row, reg + WAVE_HDR,
                                                                              (int*)reg, nullptr);
     }
+}
+
+template <int BYTES, bool GROUPED = false, bool HASH = false>
+__global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
+    num_wave_rows<BYTES, GROUPED, HASH>(a);
+}
+template <int BYTES>
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_HASH) void k_num_wave_hash(NumArgs a) {
+    num_wave_rows<BYTES, false, true>(a);
+}
+template <int BYTES>
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_DIRECT) void k_num_wave_direct(NumArgs a) {
+    num_wave_rows<BYTES, false, false>(a);
 }
 
 template <int T, bool GLOBALMEM>
@@ -2133,14 +2203,14 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
 }
 
 template <int W, int K>
-__global__ __launch_bounds__(256) void k_tiny_num(TinyArgs a) {
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_TINY) void k_tiny_num(TinyArgs a) {
     tiny_rows<W, K, true>(a, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // Every symbolic tiny class in one launch (the bins' sizes are on the device): blocks
 // [TINY_SYM_GRID*c, TINY_SYM_GRID*(c+1)) walk class c's list.
 constexpr int TINY_SYM_GRID = 1024;
-__global__ __launch_bounds__(256) void k_tiny_sym(TinyArgs a) {
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_tiny_sym(TinyArgs a) {
     const int c = (int)blockIdx.x / TINY_SYM_GRID, bid = (int)blockIdx.x % TINY_SYM_GRID;
     static_assert(TINY_NC == 6 && tiny_w(0) == 8 && tiny_k(0) == 1 && tiny_w(1) == 32 && tiny_k(1) == 1 &&
                       tiny_w(2) == 32 && tiny_k(2) == 2 && tiny_w(3) == 32 && tiny_k(3) == 4 &&
@@ -2232,10 +2302,10 @@ hipError_t init_kernel_attributes() {
         e = hipFuncSetAttribute((const void*)k_num_block<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 LDS_MAX);
     if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                LDS_MAX);
+        e = hipFuncSetAttribute((const void*)k_num_wave_direct<NUM_W16_BYTES>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES, false, true>,
+        e = hipFuncSetAttribute((const void*)k_num_wave_hash<NUM_W16_BYTES>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES, true>,
@@ -2374,19 +2444,19 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
     if (h.num_count[NUM_W16H] > 0) {
         const int count = a.count = h.num_count[NUM_W16H];
         a.list = w.bin_list + (long long)(NUM_W16H - 1) * A.M;
-        hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, false, true>), dim3(round8((count + WPB - 1) / WPB, 2048)),
+        hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), dim3(round8((count + WPB - 1) / WPB, 2048)),
                            dim3(256), WPB * NUM_W16_BYTES, s, a);
     }
     if (h.num_count[NUM_WSH] > 0) {
         const int count = a.count = h.num_count[NUM_WSH];
         a.list = w.bin_list + (long long)(NUM_WSH - 1) * A.M;
-        hipLaunchKernelGGL((k_num_wave<NUM_WS_BYTES, false, true>),
-                           dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)), dim3(256), WPB * NUM_WS_BYTES, s, a);
+        hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
+                           dim3(256), WPB * NUM_WS_BYTES, s, a);
     }
     if (h.num_count[NUM_W16] > 0) {
         const int count = a.count = h.num_count[NUM_W16];
         a.list = w.bin_list + (long long)(NUM_W16 - 1) * A.M;
-        hipLaunchKernelGGL(k_num_wave<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
+        hipLaunchKernelGGL(k_num_wave_direct<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
                            WPB * NUM_W16_BYTES, s, a);
     }
     for (int c = TINY_NC - 1; c >= 0; --c) {
@@ -2423,8 +2493,8 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
     if (h.num_count[NUM_WS] > 0) {
         const int count = a.count = h.num_count[NUM_WS];
         a.list = w.bin_list + (long long)(NUM_WS - 1) * A.M;
-        hipLaunchKernelGGL(k_num_wave<NUM_WS_BYTES>, dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)), dim3(256),
-                           WPB * NUM_WS_BYTES, s, a);
+        hipLaunchKernelGGL(k_num_wave_direct<NUM_WS_BYTES>, dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
+                           dim3(256), WPB * NUM_WS_BYTES, s, a);
     }
 }
 
