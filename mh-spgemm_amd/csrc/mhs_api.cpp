@@ -192,15 +192,6 @@ int ensure(mhs_ctx* ctx, char** buf, size_t* have, size_t need) {
 
 constexpr int NUM_GLOBAL_GRID = 128;
 
-int sym_global_grid(int N, size_t* bytes) {
-    const size_t per = sym_global_bytes_per_block(N);
-    size_t g = per ? (size_t)(256u << 20) / per : 64;
-    if (g < 1) g = 1;
-    if (g > 64) g = 64;
-    if (g >= 8) g &= ~size_t(7);
-    *bytes = g * per;
-    return (int)g;
-}
 
 }  // namespace
 
@@ -315,11 +306,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
 
     // ---- mem_alloc: workspace (cached across calls) + C.ptr --------------------
     const Layout L = plan(M, MB, A->nnz, B->nnz);
-    size_t sym_g_bytes = 0;
-    const int sym_grid = sym_global_grid(N, &sym_g_bytes);
     int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
-    if (rc) return rc;
-    rc = ensure(ctx, &ctx->gscratch, &ctx->gscratch_bytes, sym_g_bytes);
     if (rc) return rc;
     MHS_HIP(pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4));
     Work w{};
@@ -364,7 +351,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // ---- Calculate_C_nnz ------------------------------------------------------------
     // persistent grids that read their bins' sizes on the device: no host round trip
     launch_symbolic_common(a, b, w, M, N, out.ptr, s);
-    launch_symbolic_rare(a, w, M, N, out.ptr, s, sym_grid);
+    launch_symbolic_rare(a, w, M, N, out.ptr, s);
     MHS_HIP(hipGetLastError());
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------

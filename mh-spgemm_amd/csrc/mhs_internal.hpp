@@ -266,7 +266,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
 int analyze_blocks(long long nnzA, int M);
 
 void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s);
-void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid);
+void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s);
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
                           Published* pub, int seq);
 void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,

@@ -1287,6 +1287,26 @@ __device__ __forceinline__ void clear_tiles(const Team& tm, TileEntry* E, int H)
     }
 }
 
+constexpr int WIDE_WT = 16384;  // tiles per window: 1 M columns (masks 128 KiB + bases 16 KiB)
+static_assert(WIDE_WT * 9 <= B1024_BYTES, "a wide window fits the 1024-thread kernel's LDS");
+
+// Wide-row tile walk: OR each B tile inside the window [w0, w1) into a dense mask array.
+struct WideTiles {
+    static constexpr bool kValues = false;
+    unsigned long long* masks;
+    int w0, w1;
+    const int* __restrict__ btcol;
+    const unsigned long long* __restrict__ btmask;
+    struct Item {
+        int tc;
+        unsigned long long m;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{btcol[i], btmask[i]}; }
+    __device__ __forceinline__ void put(const Item& x, double) const {
+        if (x.tc >= w0 && x.tc < w1) atomicOr(&masks[x.tc - w0], x.m);
+    }
+};
+
 // ------------------------------------------------------------- symbolic ---
 struct SymArgs {
     int M;
@@ -1396,29 +1416,65 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
 
 // Every rare symbolic bin in one launch (their sizes are on the device; an empty bin
 // costs nothing but its loop test): 1024-thread blocks holding all 160 KiB of LDS.
-//   phase 0  global-memory rows (blocks < gg, tables in global scratch),
-//   phase 1  rows for the 1024-thread block's LDS table,
+//   phase 1  rows past the 32 KiB table: direct-mapped ones in the 1024-thread block's
+//            LDS table, hashed ones and rows past the LDS as wide rows (dense windows),
 //   phase 2  rows for a 10 KiB table: a wave per row, 16 waves per block.
 // (Rows for a 32 KiB table keep a 256-thread kernel of their own: at one block per CU
 // they would have a fifth of the rows in flight.)
-__global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a, int gg) {
+// Wide rows (the hashed 1024-block rows and every row past its LDS): windows of
+// WIDE_WT tiles, a dense 64-bit mask per tile in LDS (no hash, no CAS, no global
+// table); nnz = sum of popcounts, tiles = non-zero masks.
+__device__ void sym_row_wide(const BlockTeam<1024, false>& tm, const SymArgs& a, int row, unsigned long long* masks,
+                             int4* stage) {
+    constexpr int T = 1024;
+    const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
+    const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
+    const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
+    const int a0 = __builtin_amdgcn_readfirstlane(a.Aptr[row]), a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
+    long long n = 0;
+    int t = 0;
+    for (int w0 = lo; w0 <= hi; w0 += WIDE_WT) {
+        const int w1 = min(hi + 1, w0 + WIDE_WT), wt = w1 - w0;
+        for (int sl = tm.rank(); sl < wt; sl += T) masks[sl] = 0ull;
+        tm.sync();
+        walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop, WideTiles{masks, w0, w1, a.btcol, a.btmask},
+                      stage);
+        tm.sync();
+        long long wn = 0;
+        int wtl = 0;
+        for (int sl = tm.rank(); sl < wt; sl += T) {
+            const unsigned long long m = masks[sl];
+            wn += __popcll(m);
+            wtl += m != 0ull;
+        }
+        n += tm.sum(wn);  // (sum syncs: the masks are free for the next window)
+        t += tm.sum(wtl);
+    }
+    const int R = __builtin_amdgcn_readfirstlane((int)a.grp[row]);
+    if (tm.rank() < R) {
+        a.Cptr[row + tm.rank()] = (int)n;
+        a.ctiles[row + tm.rank()] = t;
+    }
+    tm.sync();
+}
+
+__global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int4* stage = (int4*)(smem + 1024);
-    if ((int)blockIdx.x < gg) {
-        BlockTeam<1024, true> tg{(long long*)smem};
-        TileEntry* E = (TileEntry*)(a.gscratch + (long long)blockIdx.x * a.gbytes);
-        const int count = a.stats->sym_count[SYM_GLOBAL];
-        const int* list = a.list + (long long)(SYM_GLOBAL - 1) * a.M;
-        for (RowWalk rw(count, 1, 0, (int)blockIdx.x, gg); rw.first < rw.end; rw.first += rw.stride)
-            sym_row(tg, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
-    }
     BlockTeam<1024, false> tm{(long long*)smem};
     TileEntry* E = (TileEntry*)(smem + BLOCK_HDR);
-    {
-        const int count = a.stats->sym_count[SYM_B1024];
-        const int* list = a.list + (long long)(SYM_B1024 - 1) * a.M;
-        for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
-            sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
+#pragma unroll 1
+    for (int bin = SYM_GLOBAL; bin >= SYM_B1024; --bin) {
+        const int count = a.stats->sym_count[bin];
+        const int* list = a.list + (long long)(bin - 1) * a.M;
+        for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride) {
+            const int row = __builtin_amdgcn_readfirstlane(list[rw.first]);
+            const int span = __builtin_amdgcn_readfirstlane(a.rhi[row]) - __builtin_amdgcn_readfirstlane(a.rlo[row]) + 1;
+            if (bin == SYM_B1024 && sym_direct(span, __builtin_amdgcn_readfirstlane(a.rtflop[row])))
+                sym_row(tm, a, row, E, stage);
+            else
+                sym_row_wide(tm, a, row, (unsigned long long*)E, stage);
+        }
     }
     __syncthreads();  // phase 2 reuses the whole LDS
     const int w = threadIdx.x >> 6;
@@ -1850,24 +1906,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
 // products accumulate straight into the row's slice of C.val with global FP64
 // atomics (zeroed first).  A product's rank = base4[g] + popcounts of the masks of
 // the tiles before it in its group of 4 + popc(mask & below(col)).
-constexpr int WIDE_WT = 16384;  // tiles per window: 1 M columns (masks 128 KiB + bases 16 KiB)
-static_assert(WIDE_WT * 9 <= B1024_BYTES, "a wide window fits the 1024-thread kernel's LDS");
 
-struct WideTiles {
-    static constexpr bool kValues = false;
-    unsigned long long* masks;
-    int w0, w1;
-    const int* __restrict__ btcol;
-    const unsigned long long* __restrict__ btmask;
-    struct Item {
-        int tc;
-        unsigned long long m;
-    };
-    __device__ __forceinline__ Item load(int i) const { return Item{btcol[i], btmask[i]}; }
-    __device__ __forceinline__ void put(const Item& x, double) const {
-        if (x.tc >= w0 && x.tc < w1) atomicOr(&masks[x.tc - w0], x.m);
-    }
-};
 
 struct WideAccum {
     static constexpr bool kValues = true;
@@ -2382,10 +2421,10 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
 
 // The rare bins (10 KiB waves, 32 KiB and 157 KiB block tables, global memory): one
 // persistent launch that reads the bins' sizes on the device.
-void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, int global_grid) {
+void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s) {
     if (M <= 0) return;
     SymArgs a = sym_args(A, w, M, N, Cptr);
-    hipLaunchKernelGGL(k_sym_rare, dim3(std::max(256, global_grid)), dim3(1024), LDS_MAX - 1024, s, a, global_grid);
+    hipLaunchKernelGGL(k_sym_rare, dim3(256), dim3(1024), LDS_MAX - 1024, s, a);
     a.bin = SYM_B256;
     hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, 1024)), dim3(256), SYM_B256_BYTES, s, a);
 }
