@@ -1800,6 +1800,42 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
         tm.exclusive_scan(
             span, [&](int i) { return (int)__popcll(E[i].mask); },
             [&](int i, int v) { E[i].base = v; });
+    } else if (Team::size > 64 &&
+               (long long)((span + 63) >> 6) * 12 + 16 + (long long)t * 4 <= num_acc_bytes(NM_HASH, span, t, n)) {
+        // block teams, tables of many tiles: rank by a bitmap over the span instead of a
+        // sort -- bit per occupied tile, prefix popcount of the bitmap words, then a
+        // tile's rank = word prefix + popc(word & below); bases = exclusive scan of the
+        // masks' popcounts in rank order.  O(H + span/64 + t), no bitonic rounds.
+        const int nw = (span + 63) >> 6;
+        unsigned long long* bm = (unsigned long long*)acc;  // acc is free until the accumulate
+        int* wpre = (int*)(bm + nw);
+        int* cnt = wpre + ((nw + 3) & ~3);
+        for (int i = tm.rank(); i < nw; i += Team::size) bm[i] = 0ull;
+        tm.sync();
+        for (int s = tm.rank(); s < H; s += Team::size) {
+            const int key = E[s].key;
+            if (key != -1) atomicOr(&bm[(key - lo) >> 6], 1ull << ((key - lo) & 63));
+        }
+        tm.sync();
+        tm.exclusive_scan(
+            nw, [&](int i) { return (int)__popcll(bm[i]); }, [&](int i, int v) { wpre[i] = v; });
+        tm.sync();
+        auto rank_of = [&](int key) {
+            const int d = key - lo;
+            return wpre[d >> 6] + (int)__popcll(bm[d >> 6] & ((1ull << (d & 63)) - 1));
+        };
+        for (int s = tm.rank(); s < H; s += Team::size) {
+            const uint4 q = *reinterpret_cast<const uint4*>(&E[s]);
+            if ((int)q.w != -1) cnt[rank_of((int)q.w)] = __popcll(((unsigned long long)q.y << 32) | q.x);
+        }
+        tm.sync();
+        tm.exclusive_scan(
+            t, [&](int i) { return cnt[i]; }, [&](int i, int v) { cnt[i] = v; });
+        tm.sync();
+        for (int s = tm.rank(); s < H; s += Team::size) {
+            const int key = E[s].key;
+            if (key != -1) E[s].base = cnt[rank_of(key)];
+        }
     } else {
         unsigned long long* S = (unsigned long long*)acc;
         const int P = next_pow2(t);

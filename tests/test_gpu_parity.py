@@ -358,3 +358,20 @@ def test_wide_column_space_small_rows(tool):
     t = check(tool, A, B)
     assert t.sym_bins[5] + t.sym_bins[6] > 0, t.sym_bins
     assert all(t.num_bins[i] == 0 for i in range(8, 14)), t.num_bins
+
+
+@pytest.mark.parametrize("per_b", [16, 20])
+def test_block_hash_rows_rank(tool, per_b):
+    # hashed rows with ~1000 tiles over a moderate span: the 256-thread kernel ranks the
+    # tiles by a bitmap over the span instead of sorting them
+    rng = np.random.default_rng(per_b)
+    K, N = 2000, 200_000
+    Bp, Bc, Bv = random_csr(K, N, 50, seed=per_b + 1)
+    rows = [np.sort(rng.choice(K, per_b, replace=False)) for _ in range(300)]
+    Ap = np.zeros(len(rows) + 1, np.int64)
+    Ap[1:] = np.cumsum([len(r) for r in rows])
+    A = mhspgemm.CSR(len(rows), K, Ap.astype(np.int32), np.concatenate(rows).astype(np.int32),
+                     rng.uniform(0.1, 1.0, int(Ap[-1])))
+    B = mhspgemm.CSR(K, N, Bp, Bc, Bv)
+    t = check(tool, A, B)
+    assert t.num_bins[3] > 0, t.num_bins
