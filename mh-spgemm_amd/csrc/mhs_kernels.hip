@@ -1800,7 +1800,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
         tm.exclusive_scan(
             span, [&](int i) { return (int)__popcll(E[i].mask); },
             [&](int i, int v) { E[i].base = v; });
-    } else if (Team::size > 64 &&
+    } else if ((Team::size > 64 || t >= 64) &&
                (long long)((span + 63) >> 6) * 12 + 16 + (long long)t * 4 <= num_acc_bytes(NM_HASH, span, t, n)) {
         // block teams, tables of many tiles: rank by a bitmap over the span instead of a
         // sort -- bit per occupied tile, prefix popcount of the bitmap words, then a
