@@ -443,11 +443,18 @@ __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* 
     bool differ = false;
     int ntiles = 0, prev_col = -1;
     unsigned long long carry = 0;
+    // the next chunk's columns are loaded one iteration ahead (its load latency overlaps
+    // this chunk's shuffles); the chunk-edge neighbour is the next chunk's first column
+    int c_nx = s + gl < e ? col[s + gl] : INT_MAX;
+    int p_nx = (same_len && s + gl < e) ? col[ps + gl] : 0;
     for (int b = s; b < e; b += G) {
         const int j = b + gl;
         const bool in = j < e;
-        const int c = in ? col[j] : INT_MAX;
-        if (same_len && in && col[ps + (j - s)] != c) differ = true;
+        const int c = c_nx;
+        if (same_len && in && p_nx != c) differ = true;
+        c_nx = j + G < e ? col[j + G] : INT_MAX;
+        p_nx = (same_len && j + G < e) ? col[ps + (j + G - s)] : 0;
+        const int first_next = __shfl(c_nx, gbase);
         const int up = __shfl_up(c, 1, G);
         const int pc = (gl == 0) ? prev_col : up;
         const int tile = c >> TILE_SHIFT;
@@ -458,7 +465,7 @@ __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* 
         // next entry's column: within the chunk from the neighbour lane, at the
         // chunk edge from memory
         const int dn = __shfl_down(c, 1, G);
-        int nc = (gl == G - 1) ? ((j + 1 < e) ? col[j + 1] : INT_MAX) : dn;
+        int nc = (gl == G - 1) ? first_next : dn;
         if (j + 1 >= e) nc = INT_MAX;
         const bool tail = in && ((nc >> TILE_SHIFT) != tile || nc == INT_MAX);
         // forward segmented OR within the chunk
@@ -1629,6 +1636,31 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     }
     const long long inc = wave_incl_scan64(loc);
     if (lane == 63) ws[w] = inc;
+    // numeric bin of every row (independent of the prefix: its loads overlap the
+    // predecessors' publication instead of following the look-back)
+    __shared__ unsigned char nbin_of[SCAN_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = base + k;
+        int nbin = NUM_NONE;
+        if (i < M) {
+            const int n = v[k];
+            const int lo = rlo[i], hi = rhi[i];
+            const int span = n ? hi - lo + 1 : 0;
+            const int g = grp[i];
+            // a group runs as one item when its R accumulators fit a wave bin; its
+            // members decide alike (same pattern, same sizes) and then stay out
+            const int gh = (g & GRP_CONT) ? grp[i - (g & 0x7F)] : g;
+            const int nA = Aptr[i + 1] - Aptr[i];
+            const int gb = num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max, nA, tiny_ok);
+            if (gb != NUM_NONE)
+                nbin = (g & GRP_CONT) ? NUM_NONE : gb;
+            else
+                nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max, nA,
+                                  tiny_ok);
+        }
+        nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
+    }
     __syncthreads();
     long long woff = 0, total = 0;
     for (int k = 0; k < 16; ++k) {
@@ -1661,29 +1693,10 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     }
     __syncthreads();
     long long off = excl_s + woff + inc - loc;
-    __shared__ unsigned char nbin_of[SCAN_ITEMS];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = base + k;
         if (i <= M) Cptr[i] = (int)off;
-        int nbin = NUM_NONE;
-        if (i < M) {
-            const int n = v[k];
-            const int lo = rlo[i], hi = rhi[i];
-            const int span = n ? hi - lo + 1 : 0;
-            const int g = grp[i];
-            // a group runs as one item when its R accumulators fit a wave bin; its
-            // members decide alike (same pattern, same sizes) and then stay out
-            const int gh = (g & GRP_CONT) ? grp[i - (g & 0x7F)] : g;
-            const int nA = Aptr[i + 1] - Aptr[i];
-            const int gb = num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max, nA, tiny_ok);
-            if (gb != NUM_NONE)
-                nbin = (g & GRP_CONT) ? NUM_NONE : gb;
-            else
-                nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max, nA,
-                                  tiny_ok);
-        }
-        nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
         off += v[k];
     }
     __syncthreads();
