@@ -134,10 +134,16 @@ __host__ __device__ inline int ilog2(int x) {  // x power of two
     while ((1 << l) < x) ++l;
     return l;
 }
-// Open-addressed table size for up to `bound` distinct keys: load <= 2/3 (linear
-// probing stays short; a tighter table lets more rows share a CU's LDS, and the
-// small-row phases are bound by rows in flight, not by probes).
+// Open-addressed table size for up to `bound` distinct keys: load <= 2/3, rounded to
+// 16 slots, not to a power of two (slots come from a multiply-high range reduction):
+// linear probing stays short, and a tighter table lets more rows share a CU's LDS --
+// the small-row phases are bound by rows in flight, not by probes.
 __host__ __device__ inline int hash_slots(int bound) {
+    const int b = bound < 1 ? 1 : bound;
+    return (b + ((b + 1) >> 1) + 15) & ~15;  // >= ceil(1.5 b) > b: an insert always finds a slot
+}
+// the power-of-two sizing the direct/hash choice of symbolic was tuned with
+__host__ __device__ inline int hash_slots_pow2(int bound) {
     const int b = bound < 1 ? 1 : bound;
     const int h = next_pow2(b + (b >> 1) + 1);
     return h < 16 ? 16 : h;
@@ -149,7 +155,7 @@ __host__ __device__ inline long long align16(long long x) { return (x + 15) & ~1
 // does not push the row into a bigger bin than the hash would; else hashed.
 __host__ __device__ inline bool sym_direct(int span, int tflop) {
     const int bound = tflop < span ? tflop : span;
-    const int h = hash_slots(bound);
+    const int h = hash_slots_pow2(bound);
     return span <= 2 * h && (span <= h || (long long)span * 16 <= 4096);
 }
 __host__ __device__ inline long long sym_need(int span, int tflop) {
@@ -175,9 +181,14 @@ __host__ __device__ inline long long num_need_dense(int span) { return (long lon
 __host__ __device__ inline long long num_need_direct(int span, int n) {
     return (long long)span * 16 + align16((long long)n * 8);
 }
+// Hash rows rank their tiles by counting smaller keys when t <= HASH_CNT_T (t^2/64 compares
+// per wave, no sort buffer); bigger tables are bitonic-sorted in a next_pow2(t) buffer
+// that shares the accumulator region.
+constexpr int HASH_CNT_T = 192;
+__host__ __device__ inline int hash_sort_p(int t) { return t <= HASH_CNT_T ? 0 : next_pow2(t); }
 __host__ __device__ inline long long num_need_hash(int t, int n) {
     const int h = hash_slots(t);
-    const int p = next_pow2(t);
+    const int p = hash_sort_p(t);
     return (long long)h * 16 + align16((long long)(n > p ? n : p) * 8);
 }
 __host__ __device__ inline long long num_need_rmap(int span, int n) {
@@ -216,7 +227,7 @@ __host__ __device__ inline bool num_wide(int span, int t, int n, int dense_span_
 __host__ __device__ inline long long num_acc_bytes(int m, int span, int t, int n) {
     if (m == NM_DENSE) return (long long)span * 64 * 8;
     if (m == NM_HASH) {
-        const int p = next_pow2(t);
+        const int p = hash_sort_p(t);
         return align16((long long)(n > p ? n : p) * 8);
     }
     return align16((long long)n * 8);

@@ -160,9 +160,11 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
-__device__ __forceinline__ int hslot(int key, int shift) {
-    return (int)(((unsigned)key * 2654435769u) >> (32 - shift));
+// Fibonacci hash of a tile key into [0, H) (any H: multiply-high range reduction)
+__device__ __forceinline__ int hslot(int key, int H) {
+    return (int)__umulhi((unsigned)key * 2654435769u, (unsigned)H);
 }
+__device__ __forceinline__ int hnext(int s, int H) { return s + 1 < H ? s + 1 : 0; }
 
 __device__ __forceinline__ int sat_int(long long x) { return x > INT_MAX ? INT_MAX : (int)x; }
 
@@ -1156,7 +1158,7 @@ struct TileBuild {
     static constexpr bool kValues = false;
     TileEntry* E;
     bool direct;
-    int lo, H, hshift;
+    int lo, H;
     const int* __restrict__ btcol;
     const unsigned long long* __restrict__ btmask;
     struct Item {
@@ -1168,14 +1170,14 @@ struct TileBuild {
         if (direct) {
             atomicOr(&E[x.tc - lo].mask, x.m);
         } else {
-            int s = hslot(x.tc, hshift);
+            int s = hslot(x.tc, H);
             for (;;) {
                 const int old = atomicCAS(&E[s].key, -1, x.tc);
                 if (old == -1 || old == x.tc) {
                     atomicOr(&E[s].mask, x.m);
                     break;
                 }
-                s = (s + 1) & (H - 1);
+                s = hnext(s, H);
             }
         }
     }
@@ -1191,7 +1193,7 @@ struct Accum {
     const TileEntry* E;
     double* acc;
     const unsigned short* rmap;
-    int lo, H, hshift, colbase;
+    int lo, H, colbase;
     const int* __restrict__ Bcol;
     const double* __restrict__ Bval;
     struct Item {
@@ -1254,12 +1256,12 @@ struct Accum {
             if constexpr (MODE == NM_DIRECT) {
                 s = tc - lo;
             } else {
-                s = hslot(tc, hshift);
+                s = hslot(tc, H);
             }
             uint4 q = *reinterpret_cast<const uint4*>(&E[s]);  // one ds_read_b128: mask, base, key
             if constexpr (MODE == NM_HASH) {
                 while ((int)q.w != tc) {
-                    s = (s + 1) & (H - 1);
+                    s = hnext(s, H);
                     q = *reinterpret_cast<const uint4*>(&E[s]);
                 }
             }
@@ -1273,13 +1275,13 @@ struct Accum {
 
 template <class Team>
 __device__ __forceinline__ void build_tiles(const Team& tm, TileEntry* E, bool direct, int lo,
-                                            int H, int hshift, int a0, int a1,
+                                            int H, int a0, int a1,
                                             const int* __restrict__ Acol,
                                             const int4* __restrict__ bmeta,
                                             const int* __restrict__ btcol,
                                             const unsigned long long* __restrict__ btmask,
                                             int tflop, int4* stage) {
-    const TileBuild f{E, direct, lo, H, hshift, btcol, btmask};
+    const TileBuild f{E, direct, lo, H, btcol, btmask};
     walk_products(tm, a0, a1, Acol, nullptr, bmeta, true, tflop, f, stage);
 }
 
@@ -1344,10 +1346,9 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
     const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
     const bool direct = sym_direct(span, tflop);
     const int H = direct ? span : hash_slots(tflop < span ? tflop : span);
-    const int hshift = direct ? 0 : ilog2(H);
     clear_tiles(tm, E, H);
     tm.sync();
-    build_tiles(tm, E, direct, lo, H, hshift, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
+    build_tiles(tm, E, direct, lo, H, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
                 __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]), a.Acol, a.bmeta, a.btcol, a.btmask,
                 tflop, stage);
     tm.sync();
@@ -1752,7 +1753,6 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                              int4* stage, int R) {
     MHS_STAMP0();
     const int H = MODE == NM_HASH ? hash_slots(t) : span;
-    const int hshift = MODE == NM_HASH ? ilog2(H) : 0;
     const int colbase = lo << TILE_SHIFT;
     TileEntry* E = (TileEntry*)region;
     unsigned short* rmap = (unsigned short*)(region + (long long)H * 16);
@@ -1792,8 +1792,8 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             if (MODE != NM_HASH) {
                 E[key - lo].mask = m;
             } else {
-                int sl = hslot(key, hshift);
-                while (atomicCAS(&E[sl].key, -1, key) != -1) sl = (sl + 1) & (H - 1);  // keys are distinct
+                int sl = hslot(key, H);
+                while (atomicCAS(&E[sl].key, -1, key) != -1) sl = hnext(sl, H);  // keys are distinct
                 E[sl].mask = m;
             }
         }
@@ -1802,7 +1802,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
         clear_tiles(tm, E, H);
         if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
         tm.sync();
-        build_tiles(tm, E, MODE != NM_HASH, lo, H, hshift, a0, a1, a.Acol, a.bmeta, a.btcol, a.btmask,
+        build_tiles(tm, E, MODE != NM_HASH, lo, H, a0, a1, a.Acol, a.bmeta, a.btcol, a.btmask,
                     tflop, stage);
         tm.sync();
     }
@@ -1849,6 +1849,40 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             const int key = E[s].key;
             if (key != -1) E[s].base = cnt[rank_of(key)];
         }
+    } else if (t <= HASH_CNT_T || (long long)((t + Team::size - 1) / Team::size) * t <= 768) {
+        // few tiles: rank by counting.  Compact the table into (key, slot << 8 | popc)
+        // pairs (a ballot per wave, one counter add per wave), then a tile's base = the
+        // popcounts of the smaller keys summed over the list -- t compares per tile on
+        // broadcast LDS reads, no sort rounds (t <= n: the list fits the accumulator).
+        int2* L = (int2*)acc;  // acc is free until the accumulate
+        const int lane = lane_id();
+        for (int s0 = tm.rank() & ~63; s0 < H; s0 += Team::size) {
+            const int s = s0 + lane;
+            uint4 q = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
+            if (s < H) q = *reinterpret_cast<const uint4*>(&E[s]);  // mask, base, key
+            const bool occ = (int)q.w != -1;
+            const unsigned long long bal = __ballot(occ);
+            int at = 0;
+            if (lane == 0 && bal) at = atomicAdd(counter, __popcll(bal));
+            at = __shfl(at, 0);
+            if (occ)
+                L[at + __popcll(bal & lanemask_lt())] =
+                    make_int2((int)q.w, (s << 8) | __popcll(((unsigned long long)q.y << 32) | q.x));
+        }
+        tm.sync();
+        for (int i = tm.rank(); i < t; i += Team::size) {
+            const int2 me = L[i];
+            int base = 0, j = 0;
+            for (; j + 1 < t; j += 2) {  // two entries per broadcast read
+                const int4 o = *reinterpret_cast<const int4*>(&L[j]);
+                base += (o.x < me.x ? (o.y & 0xFF) : 0) + (o.z < me.x ? (o.w & 0xFF) : 0);
+            }
+            if (j < t) {
+                const int2 o = L[j];
+                base += o.x < me.x ? (o.y & 0xFF) : 0;
+            }
+            E[me.y >> 8].base = base;
+        }
     } else {
         unsigned long long* S = (unsigned long long*)acc;
         const int P = next_pow2(t);
@@ -1885,7 +1919,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
 
     // 3. accumulate every product of the row (of the group's rows)
     {
-        const Accum<GLOBALMEM, MODE> f{E, acc, rmap, lo, H, hshift, colbase, a.Bcol, a.Bval};
+        const Accum<GLOBALMEM, MODE> f{E, acc, rmap, lo, H, colbase, a.Bcol, a.Bval};
         if constexpr (GROUPED)
             for_products_group(a0, a1, a.Acol, a.Aval, a.bmeta, pick_group(a.rflop[row], a1 - a0, 64), f, R,
                                a1 - a0, stride);
@@ -1926,18 +1960,43 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                 }
             }
         } else {
-            for (int s = tm.rank(); s < H; s += Team::size) {
-                const TileEntry e = E[s];
-                unsigned long long mk = e.mask;
-                if (!mk) continue;
-                const int key = MODE != NM_HASH ? lo + s : e.key;
-                int r = c0 + e.base;
-                while (mk) {
-                    const int b = __builtin_ctzll(mk);
-                    for (int g = 0; g < (GROUPED ? R : 1); ++g) a.Ccol[r + g * n] = (key << TILE_SHIFT) + b;
-                    ++r;
-                    mk &= mk - 1;
+            // column indices through LDS (the accumulator is free once the values are
+            // out): a lane expands its tile's bits, tiles of more than 8 bits are expanded
+            // by the whole wave (lane = bit); then one coalesced copy to C.col
+            tm.sync();
+            int* cb = (int*)acc;
+            const int lane = lane_id();
+            for (int s0 = tm.rank() & ~63; s0 < H; s0 += Team::size) {
+                const int s = s0 + lane;
+                unsigned long long mk = 0;
+                int key = 0, base = 0;
+                if (s < H) {
+                    const TileEntry e = E[s];
+                    mk = e.mask;
+                    key = MODE != NM_HASH ? lo + s : e.key;
+                    base = e.base;
                 }
+                const bool big = __popcll(mk) > 8;
+                unsigned long long bigs = __ballot(big);
+                if (!big) {
+                    int r = base;
+                    while (mk) {
+                        cb[r++] = (key << TILE_SHIFT) + __builtin_ctzll(mk);
+                        mk &= mk - 1;
+                    }
+                }
+                while (bigs) {
+                    const int src = __builtin_ctzll(bigs);
+                    bigs &= bigs - 1;
+                    const unsigned long long m2 = __shfl(mk, src);
+                    const int k2 = __shfl(key, src), b2 = __shfl(base, src);
+                    if ((m2 >> lane) & 1ull) cb[b2 + __popcll(m2 & lanemask_lt())] = (k2 << TILE_SHIFT) + lane;
+                }
+            }
+            tm.sync();
+            for (int r = tm.rank(); r < n; r += Team::size) {
+                const int c = cb[r];
+                for (int g = 0; g < (GROUPED ? R : 1); ++g) a.Ccol[c0 + g * n + r] = c;
             }
         }
     }

@@ -32,3 +32,9 @@ slow = heads & (tot_r >= thr)
 print("slowest 1%% rows: %d rows, mean total %.0f cycles" % (slow.sum(), tot_r[slow].mean()))
 for k, nm in enumerate(names):
     print(f"  {nm:20s} {ph[slow, k].mean():10.0f} cycles/row")
+# the bulk: rows between the 25th and 75th percentile of total cycles
+lo_, hi_ = np.percentile(tot_r[heads], [25, 75])
+mid = heads & (tot_r >= lo_) & (tot_r <= hi_)
+print("middle 50%% rows: %d rows, mean total %.0f cycles" % (mid.sum(), tot_r[mid].mean()))
+for k, nm in enumerate(names):
+    print(f"  {nm:20s} {ph[mid, k].mean():10.0f} cycles/row")
