@@ -44,6 +44,7 @@ struct mhs_ctx {
     // MHS_OPT_NUMERIC_EVENTS: ring of (start, end) events around the numeric phase
     std::vector<hipEvent_t> nev;
     long long ncalls = 0;
+    int mc_list = 0;         // tile-list cap of the row cache (0: mc_list_for(M); MHS_MC_LIST)
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays)
@@ -145,7 +146,7 @@ struct Layout {
         stats, blkflop, total;
 };
 
-Layout plan(int M, int MB, long long nnzA, long long nnzB) {
+Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list) {
     Layout L{};
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -171,7 +172,7 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB) {
     L.bin_list = take((size_t)(NUM_NB - 1) * M * 4);
     L.blkflop = take(((size_t)analyze_blocks(nnzA, M) + 1) * 8);
     L.scan_part = take(nscan * 8);
-    L.mcache = take((size_t)M * MCACHE_SPAN * 8);
+    L.mcache = take((size_t)M * mc_stride(mc_list) * 8);
     L.total = o;
     return L;
 }
@@ -221,6 +222,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     ctx->stream = ctx->own_stream;
     if (const char* e = getenv("MHS_DENSE_SPAN")) ctx->dense_span_max = atoi(e);
     if (getenv("MHS_NO_MCACHE")) ctx->use_mcache = false;
+    if (const char* e = getenv("MHS_MC_LIST")) ctx->mc_list = atoi(e) < MC_LIST_MIN ? MC_LIST_MIN : atoi(e);
     if (getenv("MHS_NO_GROUPS")) ctx->groups = false;
     *out = ctx;
     return MHS_OK;
@@ -305,7 +307,8 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     out.N = N;
 
     // ---- mem_alloc: workspace (cached across calls) + C.ptr --------------------
-    const Layout L = plan(M, MB, A->nnz, B->nnz);
+    const int mc_list = ctx->mc_list > 0 ? ctx->mc_list : mc_list_for(M);
+    const Layout L = plan(M, MB, A->nnz, B->nnz, mc_list);
     int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
     if (rc) return rc;
     MHS_HIP(pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4));
@@ -329,6 +332,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     w.nflop = M > 0 ? analyze_blocks(A->nnz, M) : 0;
     w.scan_part = (int*)(ctx->ws + L.scan_part);
     w.mcache = ctx->use_mcache ? (unsigned long long*)(ctx->ws + L.mcache) : nullptr;
+    w.mc_list = mc_list;
     w.stats = (Stats*)(ctx->ws + L.stats);
     w.gscratch = ctx->gscratch;
     w.gscratch_bytes = ctx->gscratch_bytes;

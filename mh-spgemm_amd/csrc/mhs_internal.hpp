@@ -196,11 +196,24 @@ __host__ __device__ inline long long num_need_rmap(int span, int n) {
 }
 // symbolic stores the OR'd tile masks of rows it tabled direct-mapped over a narrow span
 __host__ __device__ inline bool mcached(int span, int tflop) { return span <= MCACHE_SPAN && sym_direct(span, tflop); }
-// ... and of the other rows with at most MC_LIST distinct tiles, a compact list in the same
-// 256-byte slot: masks at [0, 16), tile keys (int32) in the next 64 bytes
-constexpr int MC_LIST = 16;
-static_assert(MC_LIST * 12 <= MCACHE_SPAN * 8, "the tile list fits the row's cache slot");
-__host__ __device__ inline bool mlisted(int span, int tflop, int t) { return !mcached(span, tflop) && t <= MC_LIST; }
+// ... and of the other rows with at most `list` distinct tiles (a run-time cap, MC_LIST_MAX
+// unless M rows of that would not fit MC_BYTES_MAX), an unordered compact list in the
+// row's slot of mc_stride(list) words: masks at [0, list), tile keys (int32) after them.
+// Numeric then skips the tile walk (and, hashed, the table compaction).
+constexpr int MC_LIST_MIN = 16;
+constexpr int MC_LIST_MAX = 128;
+constexpr long long MC_BYTES_MAX = 12LL << 30;
+__host__ __device__ inline int mc_stride(int list) {
+    const int w = list + (list + 1) / 2;
+    return w > MCACHE_SPAN ? w : MCACHE_SPAN;
+}
+inline int mc_list_for(long long M) {
+    return M * mc_stride(MC_LIST_MAX) * 8 <= MC_BYTES_MAX ? MC_LIST_MAX : MC_LIST_MIN;
+}
+static_assert(MC_LIST_MIN * 12 <= MCACHE_SPAN * 8, "the smallest tile list fits the narrow rows' slot");
+__host__ __device__ inline bool mlisted(int span, int tflop, int t, int list) {
+    return !mcached(span, tflop) && t <= list;
+}
 __host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_max) {
     if (span <= dense_span_max) return NM_DENSE;
     if (span <= RMAP_SPAN_MAX) return NM_RMAP;
@@ -266,7 +279,8 @@ struct Work {
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count
     int* scan_part;    // k_scan's look-back state: one 64-bit word per block (flag | prefix)
-    unsigned long long* mcache;   // [M][MCACHE_SPAN] tile masks of narrow rows (symbolic -> numeric)
+    unsigned long long* mcache;   // [M][mc_stride] tile masks / tile lists (symbolic -> numeric)
+    int mc_list;                  // list cap (see mlisted)
     Stats* stats;
     void* gscratch;    // global-bin scratch
     size_t gscratch_bytes;

@@ -1336,6 +1336,7 @@ struct SymArgs {
     char* gscratch;
     long long gbytes;  // per block
     unsigned long long* mcache;
+    int mc_list, mc_stride;  // row cache: tile-list cap, words per row
 };
 
 template <class Team>
@@ -1370,10 +1371,10 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
     const int r_ = tm.rank();
     if (direct && span <= MCACHE_SPAN && r_ < span && a.mcache) {
         const unsigned long long m = E[r_].mask;
-        for (int g = 0; g < R; ++g) a.mcache[(size_t)(row + g) * MCACHE_SPAN + r_] = m;
+        for (int g = 0; g < R; ++g) a.mcache[(size_t)(row + g) * a.mc_stride + r_] = m;
     }
     // ... and the compacted (key, mask) list of the other rows with few tiles
-    if (a.mcache && mlisted(span, tflop, t) && r_ < 64) {  // the first wave compacts the table
+    if (a.mcache && mlisted(span, tflop, t, a.mc_list) && r_ < 64) {  // the first wave compacts the table
         const int lane = lane_id();
         int k = 0;
         for (int s0 = 0; s0 < H; s0 += 64) {
@@ -1386,9 +1387,9 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
                 const int pos = k + __popcll(bal & lanemask_lt());
                 const int key = direct ? lo + sl : (int)q.w;
                 for (int g = 0; g < R; ++g) {
-                    unsigned long long* slot = a.mcache + (size_t)(row + g) * MCACHE_SPAN;
+                    unsigned long long* slot = a.mcache + (size_t)(row + g) * a.mc_stride;
                     slot[pos] = ((unsigned long long)q.y << 32) | q.x;
-                    reinterpret_cast<int*>(slot + MC_LIST)[pos] = key;
+                    reinterpret_cast<int*>(slot + a.mc_list)[pos] = key;
                 }
             }
             k += __popcll(bal);
@@ -1433,14 +1434,16 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
 // WIDE_WT tiles, a dense 64-bit mask per tile in LDS (no hash, no CAS, no global
 // table); nnz = sum of popcounts, tiles = non-zero masks.
 __device__ void sym_row_wide(const BlockTeam<1024, false>& tm, const SymArgs& a, int row, unsigned long long* masks,
-                             int4* stage) {
+                             int4* stage, int* lctr) {
     constexpr int T = 1024;
     const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
     const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
     const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
     const int a0 = __builtin_amdgcn_readfirstlane(a.Aptr[row]), a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
+    const int R = __builtin_amdgcn_readfirstlane((int)a.grp[row]);
     long long n = 0;
     int t = 0;
+    if (tm.rank() == 0) *lctr = 0;
     for (int w0 = lo; w0 <= hi; w0 += WIDE_WT) {
         const int w1 = min(hi + 1, w0 + WIDE_WT), wt = w1 - w0;
         for (int sl = tm.rank(); sl < wt; sl += T) masks[sl] = 0ull;
@@ -1448,6 +1451,27 @@ __device__ void sym_row_wide(const BlockTeam<1024, false>& tm, const SymArgs& a,
         walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop, WideTiles{masks, w0, w1, a.btcol, a.btmask},
                       stage);
         tm.sync();
+        if (a.mcache) {
+            // the row's tile list for numeric (complete when the row ends with t <= the cap:
+            // numeric's mlisted); unordered, a counter add per wave and window
+            const int lane = lane_id();
+            for (int s0 = tm.rank() & ~63; s0 < wt; s0 += T) {
+                const int sl = s0 + lane;
+                const unsigned long long m = sl < wt ? masks[sl] : 0ull;
+                const unsigned long long bal = __ballot(m != 0ull);
+                if (!bal) continue;
+                int at = 0;
+                if (lane == 0) at = atomicAdd(lctr, __popcll(bal));
+                at = __shfl(at, 0);
+                const int pos = at + __popcll(bal & lanemask_lt());
+                if (m && pos < a.mc_list)
+                    for (int g = 0; g < R; ++g) {
+                        unsigned long long* slot = a.mcache + (size_t)(row + g) * a.mc_stride;
+                        slot[pos] = m;
+                        reinterpret_cast<int*>(slot + a.mc_list)[pos] = w0 + sl;
+                    }
+            }
+        }
         long long wn = 0;
         int wtl = 0;
         for (int sl = tm.rank(); sl < wt; sl += T) {
@@ -1458,7 +1482,6 @@ __device__ void sym_row_wide(const BlockTeam<1024, false>& tm, const SymArgs& a,
         n += tm.sum(wn);  // (sum syncs: the masks are free for the next window)
         t += tm.sum(wtl);
     }
-    const int R = __builtin_amdgcn_readfirstlane((int)a.grp[row]);
     if (tm.rank() < R) {
         a.Cptr[row + tm.rank()] = (int)n;
         a.ctiles[row + tm.rank()] = t;
@@ -1481,7 +1504,7 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
             if (bin == SYM_B1024 && sym_direct(span, __builtin_amdgcn_readfirstlane(a.rtflop[row])))
                 sym_row(tm, a, row, E, stage);
             else
-                sym_row_wide(tm, a, row, (unsigned long long*)E, stage);
+                sym_row_wide(tm, a, row, (unsigned long long*)E, stage, (int*)(smem + 512));
         }
     }
     __syncthreads();  // phase 2 reuses the whole LDS
@@ -1745,6 +1768,7 @@ struct NumArgs {
     long long gbytes;
     int dense_span_max;
     const unsigned long long* mcache;
+    int mc_list, mc_stride;  // row cache: tile-list cap, words per row
 };
 
 template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
@@ -1770,33 +1794,43 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     // symbolic kept the masks unless it sorted the row as a tiny one (numeric runs those
     // with tables when the tiny classes are off: N beyond the packed keys' 23 bits)
     const bool sym_tiny = tiny_class(__builtin_amdgcn_readfirstlane(a.rflop[row]), a1 - a0, TINY_SYM_NC) >= 0;
+    // hashed rows rank their tiles by a bitmap over the span (block teams / many tiles,
+    // when it fits the accumulator), else by counting (few tiles), else by a sort
+    const bool rank_bitmap = MODE == NM_HASH && (Team::size > 64 || t >= 64) &&
+                             (long long)((span + 63) >> 6) * 12 + 16 + (long long)t * 4 <=
+                                 num_acc_bytes(NM_HASH, span, t, n);
+    const bool rank_count = MODE == NM_HASH && !rank_bitmap &&
+                            (t <= HASH_CNT_T || (long long)((t + Team::size - 1) / Team::size) * t <= 768);
+    bool have_list = false;  // the count list is already in acc
     if (MODE != NM_HASH && a.mcache && mcached(span, tflop) && !sym_tiny) {
         for (int s = tm.rank(); s < span; s += Team::size) {
             TileEntry z;
-            z.mask = a.mcache[(size_t)row * MCACHE_SPAN + s];
+            z.mask = a.mcache[(size_t)row * a.mc_stride + s];
             z.base = 0;
             z.key = -1;
             E[s] = z;
         }
         tm.sync();
-    } else if (a.mcache && mlisted(span, tflop, t) && !sym_tiny) {
-        // symbolic's compacted list: t <= 16 (key, mask) pairs, one per lane
+    } else if (a.mcache && mlisted(span, tflop, t, a.mc_list) && !sym_tiny) {
+        // symbolic's compacted list of the t (key, mask) pairs; a hashed row that ranks by
+        // counting also gets its (key, slot | popc) list here, no table compaction later
         clear_tiles(tm, E, H);
         if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
         tm.sync();
-        const int r = tm.rank();
-        if (r < t) {
-            const unsigned long long* slot = a.mcache + (size_t)row * MCACHE_SPAN;
+        const unsigned long long* slot = a.mcache + (size_t)row * a.mc_stride;
+        for (int r = tm.rank(); r < t; r += Team::size) {
             const unsigned long long m = slot[r];
-            const int key = reinterpret_cast<const int*>(slot + MC_LIST)[r];
+            const int key = reinterpret_cast<const int*>(slot + a.mc_list)[r];
             if (MODE != NM_HASH) {
                 E[key - lo].mask = m;
             } else {
                 int sl = hslot(key, H);
                 while (atomicCAS(&E[sl].key, -1, key) != -1) sl = hnext(sl, H);  // keys are distinct
                 E[sl].mask = m;
+                if (rank_count) reinterpret_cast<int2*>(acc)[r] = make_int2(key, (sl << 8) | __popcll(m));
             }
         }
+        have_list = MODE == NM_HASH && rank_count;
         tm.sync();
     } else {
         clear_tiles(tm, E, H);
@@ -1813,8 +1847,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
         tm.exclusive_scan(
             span, [&](int i) { return (int)__popcll(E[i].mask); },
             [&](int i, int v) { E[i].base = v; });
-    } else if ((Team::size > 64 || t >= 64) &&
-               (long long)((span + 63) >> 6) * 12 + 16 + (long long)t * 4 <= num_acc_bytes(NM_HASH, span, t, n)) {
+    } else if (rank_bitmap) {
         // block teams, tables of many tiles: rank by a bitmap over the span instead of a
         // sort -- bit per occupied tile, prefix popcount of the bitmap words, then a
         // tile's rank = word prefix + popc(word & below); bases = exclusive scan of the
@@ -1849,14 +1882,14 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             const int key = E[s].key;
             if (key != -1) E[s].base = cnt[rank_of(key)];
         }
-    } else if (t <= HASH_CNT_T || (long long)((t + Team::size - 1) / Team::size) * t <= 768) {
+    } else if (rank_count) {
         // few tiles: rank by counting.  Compact the table into (key, slot << 8 | popc)
         // pairs (a ballot per wave, one counter add per wave), then a tile's base = the
         // popcounts of the smaller keys summed over the list -- t compares per tile on
         // broadcast LDS reads, no sort rounds (t <= n: the list fits the accumulator).
         int2* L = (int2*)acc;  // acc is free until the accumulate
         const int lane = lane_id();
-        for (int s0 = tm.rank() & ~63; s0 < H; s0 += Team::size) {
+        for (int s0 = tm.rank() & ~63; !have_list && s0 < H; s0 += Team::size) {
             const int s = s0 + lane;
             uint4 q = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
             if (s < H) q = *reinterpret_cast<const uint4*>(&E[s]);  // mask, base, key
@@ -2500,6 +2533,8 @@ static SymArgs sym_args(const Csr& A, const Work& w, int M, int N, int* Cptr) {
     a.gscratch = (char*)w.gscratch;
     a.gbytes = (long long)sym_global_bytes_per_block(N);
     a.mcache = w.mcache;
+    a.mc_list = w.mc_list;
+    a.mc_stride = mc_stride(w.mc_list);
     a.bin = 0;
     return a;
 }
@@ -2550,6 +2585,8 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
     NumArgs a;
     a.dense_span_max = dense_span_max;
     a.mcache = w.mcache;
+    a.mc_list = w.mc_list;
+    a.mc_stride = mc_stride(w.mc_list);
     a.Aptr = A.ptr;
     a.Acol = A.col;
     a.Aval = A.val;

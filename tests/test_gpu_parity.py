@@ -375,3 +375,25 @@ def test_block_hash_rows_rank(tool, per_b):
     B = mhspgemm.CSR(K, N, Bp, Bc, Bv)
     t = check(tool, A, B)
     assert t.num_bins[3] > 0, t.num_bins
+
+
+@pytest.mark.parametrize("spread", [1, 40])
+def test_wide_symbolic_rows_few_tiles(tool, spread):
+    # rows with thousands of tile products over a ~31 k-tile span but only a few distinct
+    # tiles: symbolic counts them as wide rows (dense windows, two of them), numeric hashes
+    # them from the tile list symbolic leaves -- the list must span the windows
+    K, N = 3000, 2_000_000
+    k = np.arange(K)
+    first = (k % spread) * 50_000 + (k % 7)
+    last = 1_999_000 + (k % 64)
+    Bp = np.arange(0, 2 * K + 1, 2, dtype=np.int32)
+    Bc = np.stack([first, last], 1).reshape(-1).astype(np.int32)
+    rng = np.random.default_rng(spread)
+    B = mhspgemm.CSR(K, N, Bp, Bc, rng.uniform(0.5, 1.5, 2 * K))
+    rows = [np.arange(K)] * 3 + [np.sort(rng.choice(K, 2000, replace=False)) for _ in range(3)]
+    Ap = np.zeros(len(rows) + 1, np.int64)
+    Ap[1:] = np.cumsum([len(r) for r in rows])
+    A = mhspgemm.CSR(len(rows), K, Ap.astype(np.int32), np.concatenate(rows).astype(np.int32),
+                     rng.uniform(0.1, 1.0, int(Ap[-1])))
+    t = check(tool, A, B)
+    assert t.sym_bins[3] + t.sym_bins[4] > 0, t.sym_bins
