@@ -699,6 +699,12 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
 // to its lane groups with shuffles, a block through a 1 KiB LDS stage.  Each
 // lane issues two independent B loads before consuming them.
 
+// Keep a load unconditional: without a use hipcc sinks a load whose value is only
+// selected under a lane predicate into a branch, with an s_waitcnt vmcnt(0) there.
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(int& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(unsigned long long& x) { asm volatile("" : "+v"(x)); }
+
 template <class F>
 __device__ __forceinline__ void run_segment(const F& f, int s, int n, int gl, int G, double a) {
     constexpr int U = MHS_TILE_UNROLL;
@@ -710,12 +716,21 @@ __device__ __forceinline__ void run_segment(const F& f, int s, int n, int gl, in
 #pragma unroll
         for (int u = 0; u < U; ++u) f.put(x[u], a);
     }
-    for (; q < n; q += G) f.put(f.load(s + q), a);
+    if (q < n) {  // the tail (< U entries) in one batch: clamped loads, no per-entry round trip
+        typename F::Item x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = f.load(s + (q + u * G < n ? q + u * G : q));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            pin(x[u].tc);
+            pin(x[u].m);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q + u * G < n) f.put(x[u], a);
+    }
 }
 
-// Keep a load unconditional: without a use hipcc sinks a load whose value is only
-// selected under a lane predicate into a branch, with an s_waitcnt vmcnt(0) there.
-__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
 
 // Value walk over one run of LM (compile-time bound) B rows, L (<= LM) of them
 // live: B entry q of row k+i is s + i*n + q.  Loads of dead rows are clamped to
@@ -767,39 +782,33 @@ __device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl
     }
     return;
 #endif
-    int q = gl;
-    for (; q + (U - 1) * G < n; q += U * G) {
+    // U entries per lane per batch, a short segment's tail included: indices past the
+    // segment are clamped to the batch's first entry (a cache hit, not accumulated), so
+    // a segment of <= U*G entries costs one load round trip, not one per entry
+    for (int q0 = gl; q0 < n; q0 += U * G) {
         int c[U];
         double b[U][LM];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            c[u] = f.col(s + q + u * G);
+            const int q = q0 + u * G < n ? q0 + u * G : q0;
+            c[u] = f.col(s + q);
 #pragma unroll
-            for (int i = 0; i < LM; ++i) b[u][i] = f.val(s + o[i] + q + u * G);
+            for (int i = 0; i < LM; ++i) b[u][i] = f.val(s + o[i] + q);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) {
+            pin(c[u]);
 #pragma unroll
-            for (int i = 1; i < LM; ++i) pin(b[u][i]);
+            for (int i = 0; i < LM; ++i) pin(b[u][i]);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (q0 + u * G >= n) break;
             double v = a[0] * b[u][0];
 #pragma unroll
             for (int i = 1; i < LM; ++i) v += i < L ? a[i] * b[u][i] : 0.0;
             f.add(c[u], v);
         }
-    }
-    for (; q < n; q += G) {
-        const int c = f.col(s + q);
-        double b[LM];
-#pragma unroll
-        for (int i = 0; i < LM; ++i) b[i] = f.val(s + o[i] + q);
-#pragma unroll
-        for (int i = 1; i < LM; ++i) pin(b[i]);
-        double v = a[0] * b[0];
-#pragma unroll
-        for (int i = 1; i < LM; ++i) v += i < L ? a[i] * b[i] : 0.0;
-        f.add(c, v);
     }
 }
 
