@@ -128,6 +128,12 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
 template <class V>
 __device__ __forceinline__ V wave_sum(V v) {
 #pragma unroll
@@ -955,6 +961,49 @@ __device__ __forceinline__ void for_products_group(int a0, int a1, const int* __
     }
 }
 
+// A staged sub-chunk walked flattened: its nloc visits' B segments laid end to end
+// (e[v] = {B start, length, A index, inclusive prefix of the lengths}), product p of
+// tot to thread p mod T; the visit of p by a binary search of the prefixes in LDS.
+// U products per thread issue their loads together (clamped, not branched around).
+template <int T, class F>
+__device__ __forceinline__ void flat_chunk(const F& f, const int4* e, int nloc, int tot,
+                                           const double* __restrict__ Aval) {
+    constexpr int U = 2;
+    for (int p0 = threadIdx.x; p0 < tot; p0 += U * T) {
+        typename F::Item x[U];
+        int own[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int p = p0 + u * T < tot ? p0 + u * T : p0;
+            int lo = 0, hi = nloc - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (e[mid].w > p) hi = mid;
+                else lo = mid + 1;
+            }
+            const int4 v = e[lo];
+            own[u] = v.z;
+            x[u] = f.load(v.x + p - (v.w - v.y));
+        }
+        double a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (F::kValues) {
+                a[u] = Aval[own[u]];
+                pin(x[u].c);
+                pin(x[u].v);
+            } else {
+                a[u] = 0.0;
+                pin(x[u].tc);
+                pin(x[u].m);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (p0 + u * T < tot) f.put(x[u], a[u]);
+    }
+}
+
 template <int T, bool GM, class F>
 __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, int a1,
                                              const int* __restrict__ Acol,
@@ -976,9 +1025,17 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
             const StagedChunk x = stage_chunk(lane, jb, a1, Acol, nullptr, bmeta, tiles);
             const int h = x.src;
             const int st = __shfl(x.st, h), ln = __shfl(x.ln, h), L = __shfl(x.L, h);
-            if (lane < x.nh) sg[1 + lane] = make_int4(st, ln, jb + h, L);
             const int G = (F::kValues && x.lmax > 1 && Grow < MHS_RUN_GMIN) ? MHS_RUN_GMIN : Grow;
-            if (lane == 0) sg[0] = make_int4(jb < a1 ? x.nh : 0, x.lmax, G, 0);
+            // skewed chunk (no runs; its longest B segment is over twice a lane group's
+            // fair share, e.g. a hub row among short ones): walk it flattened instead
+            const int lnv = lane < x.nh ? ln : 0;
+            const int incl = wave_incl_scan(lnv);
+            const int tot = __shfl(incl, 63);
+            const int mx = wave_max(lnv);
+            const int ngrp = T / G < x.nh ? T / G : x.nh;
+            const bool flat = T <= 256 && x.lmax == 1 && ngrp > 1 && (long long)mx * ngrp > 2LL * tot;
+            if (lane < x.nh) sg[1 + lane] = make_int4(st, ln, jb + h, flat ? incl : L);
+            if (lane == 0) sg[0] = make_int4(jb < a1 ? x.nh : 0, x.lmax, G, flat ? tot : -1);
         }
         __syncthreads();
         for (int sc = 0; sc < S; ++sc) {
@@ -986,6 +1043,12 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
             const int4 hd = sg[0];
             const int nloc = hd.x, lmax = hd.y, G = hd.z;
             if (nloc == 0) break;  // sub-chunks past the row's end are empty (and all later ones)
+            if constexpr (T <= 256) {  // (the 1024-thread kernels would spill)
+                if (hd.w >= 0) {
+                    flat_chunk<T>(f, sg + 1, nloc, hd.w, Aval);
+                    continue;
+                }
+            }
             const int gs = 31 - __clz(G);  // G is a power of two
             const int grp = threadIdx.x >> gs, gl = threadIdx.x & (G - 1), ngrp = T >> gs;  // ngrp <= 64
             const int iters = (nloc + ngrp - 1) / ngrp;

@@ -38,3 +38,13 @@ mid = heads & (tot_r >= lo_) & (tot_r <= hi_)
 print("middle 50%% rows: %d rows, mean total %.0f cycles" % (mid.sum(), tot_r[mid].mean()))
 for k, nm in enumerate(names):
     print(f"  {nm:20s} {ph[mid, k].mean():10.0f} cycles/row")
+# rows grouped by product count (flop) bucket
+blen = np.diff(A.ptr).astype(np.int64)
+rf = np.add.reduceat(blen[A.col], A.ptr[:-1]) * (np.diff(A.ptr) > 0)
+edges = [0, 256, 1024, 2048, 4096, 8192, 1 << 40]
+for a_, b_ in zip(edges[:-1], edges[1:]):
+    sel = heads & (rf >= a_) & (rf < b_)
+    if sel.sum() == 0:
+        continue
+    print("flop [%d, %d): %d rows, mean total %.0f cycles:" % (a_, b_, sel.sum(), tot_r[sel].mean()),
+          " ".join(f"{nm.split('(')[0]}={ph[sel, k].mean():.0f}" for k, nm in enumerate(names)))
