@@ -1732,6 +1732,16 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     }
     const long long inc = wave_incl_scan64(loc);
     if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    long long woff = 0, total = 0;
+    for (int k = 0; k < 16; ++k) {
+        woff += k < w ? ws[k] : 0;
+        total += ws[k];
+    }
+    // the block's aggregate goes out first: successors' look-backs need it
+    if (threadIdx.x == 0 && bid > 0)
+        __hip_atomic_store(&state[bid], LB_AGG | (unsigned long long)total, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     // numeric bin of every row (independent of the prefix: its loads overlap the
     // predecessors' publication instead of following the look-back)
     __shared__ unsigned char nbin_of[SCAN_ITEMS];
@@ -1758,33 +1768,43 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
     }
     __syncthreads();
-    long long woff = 0, total = 0;
-    for (int k = 0; k < 16; ++k) {
-        woff += k < w ? ws[k] : 0;
-        total += ws[k];
-    }
-    if (threadIdx.x == 0) {
+    if (w == 0) {
+        // wave 0 looks back over 64 predecessors per round trip: lane l reads block j - l;
+        // the nearest inclusive prefix ends the walk, the aggregates above it are summed
+        // (a window with an unpublished block before that point is re-read)
         long long ex = 0;
         if (bid > 0) {
-            __hip_atomic_store(&state[bid], LB_AGG | (unsigned long long)total, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            for (int j = bid - 1;;) {
-                const unsigned long long st = __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (st == 0) {
+            // fast path (big grids: the predecessor is usually done): one load
+            unsigned long long s1 = 0;
+            if (lane == 0) s1 = __hip_atomic_load(&state[bid - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s1 = __shfl(s1, 0);
+            for (int j = bid - 1; !(s1 & LB_INC);) {
+                const int idx = j - lane;
+                const unsigned long long st =
+                    idx >= 0 ? __hip_atomic_load(&state[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : LB_INC;  // before block 0: an inclusive prefix of 0
+                const unsigned long long inc_m = __ballot((st & LB_INC) != 0);
+                const unsigned long long zero_m = __ballot(st == 0);
+                const int fi = inc_m ? __builtin_ctzll(inc_m) : 64;
+                const unsigned long long upto = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
+                if (zero_m & upto) {
                     __builtin_amdgcn_s_sleep(1);
-                    continue;  // predecessor running: its aggregate comes without waiting on us
+                    continue;  // a predecessor running: its aggregate comes without waiting on us
                 }
-                ex += (long long)(st & LB_VAL);
-                if (st & LB_INC) break;
-                --j;
+                ex += wave_sum(lane <= fi ? (long long)(st & LB_VAL) : 0LL);
+                if (fi < 64) break;
+                j -= 64;
             }
+            if (s1 & LB_INC) ex = (long long)(s1 & LB_VAL);
         }
-        __hip_atomic_store(&state[bid], LB_INC | (unsigned long long)(ex + total), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        excl_s = ex;
-        if (bid == (int)gridDim.x - 1) {
-            stats->nnzC = ex + total;
-            if (ex + total > INT_MAX) atomicOr(&stats->err, ERR_OVERFLOW);
+        if (lane == 0) {
+            __hip_atomic_store(&state[bid], LB_INC | (unsigned long long)(ex + total), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            excl_s = ex;
+            if (bid == (int)gridDim.x - 1) {
+                stats->nnzC = ex + total;
+                if (ex + total > INT_MAX) atomicOr(&stats->err, ERR_OVERFLOW);
+            }
         }
     }
     __syncthreads();
