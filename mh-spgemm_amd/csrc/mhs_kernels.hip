@@ -1470,15 +1470,16 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
     tm.sync();
 }
 
+// the small-table wave bin, blocks [0, nb) of a grid
 template <int BYTES>
-__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_wave(SymArgs a) {
+__device__ __forceinline__ void sym_wave_rows(const SymArgs& a, int bid, int nb) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int w = threadIdx.x >> 6;
     TileEntry* E = (TileEntry*)(smem + w * BYTES + WAVE_HDR);
     const int count = a.stats->sym_count[a.bin];
     const int* list = a.list + (long long)(a.bin - 1) * a.M;
     WaveTeam tm;
-    for (RowWalk rw(count, WPB, w); rw.first < rw.end; rw.first += rw.stride)
+    for (RowWalk rw(count, WPB, w, bid, nb); rw.first < rw.end; rw.first += rw.stride)
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, nullptr);
 }
 
@@ -2482,8 +2483,8 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_TINY) void k_tiny_num(Tin
 // Every symbolic tiny class in one launch (the bins' sizes are on the device): blocks
 // [TINY_SYM_GRID*c, TINY_SYM_GRID*(c+1)) walk class c's list.
 constexpr int TINY_SYM_GRID = 1024;
-__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_tiny_sym(TinyArgs a) {
-    const int c = (int)blockIdx.x / TINY_SYM_GRID, bid = (int)blockIdx.x % TINY_SYM_GRID;
+__device__ __forceinline__ void tiny_sym_rows(TinyArgs a, int blk) {
+    const int c = blk / TINY_SYM_GRID, bid = blk % TINY_SYM_GRID;
     static_assert(TINY_NC == 6 && tiny_w(0) == 8 && tiny_k(0) == 1 && tiny_w(1) == 32 && tiny_k(1) == 1 &&
                       tiny_w(2) == 32 && tiny_k(2) == 2 && tiny_w(3) == 32 && tiny_k(3) == 4 &&
                       tiny_w(4) == 64 && tiny_k(4) == 4 && tiny_w(5) == 64 && tiny_k(5) == 8 && TINY_SYM_NC == 4,
@@ -2496,6 +2497,17 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_tiny_sym(Tiny
     case 2: tiny_rows<32, 2, false>(a, bid, TINY_SYM_GRID); break;
     default: tiny_rows<32, 4, false>(a, bid, TINY_SYM_GRID); break;
     }
+}
+
+// The common symbolic bins in one launch (their sizes are on the device; an empty role
+// costs its blocks one load): blocks [0, wave_blocks) run the small-table wave bin,
+// the rest every tiny class -- one launch less, and the two overlap.
+template <int BYTES>
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_common(SymArgs a, TinyArgs t, int wave_blocks) {
+    if ((int)blockIdx.x < wave_blocks)
+        sym_wave_rows<BYTES>(a, (int)blockIdx.x, wave_blocks);
+    else
+        tiny_sym_rows(t, (int)blockIdx.x - wave_blocks);
 }
 
 // -------------------------------------------------------------- launchers ---
@@ -2638,8 +2650,7 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
     if (M <= 0) return;
     SymArgs a = sym_args(A, w, M, N, Cptr);
     a.bin = SYM_WAVE;
-    hipLaunchKernelGGL(k_sym_wave<SYM_WAVE_BYTES>, dim3(round8((M + WPB - 1) / WPB, 2048)), dim3(256),
-                       WPB * SYM_WAVE_BYTES, s, a);
+    const int wave_blocks = round8((M + WPB - 1) / WPB, 2048);
     TinyArgs t{};
     t.M = M;
     t.Aptr = A.ptr;
@@ -2651,7 +2662,8 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
     t.Cptr = Cptr;
     t.ctiles = w.ctiles;
     t.list = w.bin_list + (long long)(SYM_TINY - 1) * M;
-    hipLaunchKernelGGL(k_tiny_sym, dim3(TINY_SYM_GRID * TINY_SYM_NC), dim3(256), 0, s, t);
+    hipLaunchKernelGGL(k_sym_common<SYM_WAVE_BYTES>, dim3(wave_blocks + TINY_SYM_GRID * TINY_SYM_NC), dim3(256),
+                       WPB * SYM_WAVE_BYTES, s, a, t, wave_blocks);
 }
 
 // The rare bins (10 KiB waves, 32 KiB and 157 KiB block tables, global memory): one
