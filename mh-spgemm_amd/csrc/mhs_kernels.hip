@@ -2480,6 +2480,29 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_TINY) void k_tiny_num(Tin
     tiny_rows<W, K, true>(a, (int)blockIdx.x, (int)gridDim.x);
 }
 
+// The 32-lane-or-narrower numeric tiny classes in one launch: class f.c[k] takes blocks
+// [f.blk0[k], f.blk0[k+1]) (sizes known on the host; multiples of 8 keep the XCD walk).
+struct TinyFused {
+    int nclass;
+    int c[4];
+    int count[4];
+    int blk0[5];
+};
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(8) void k_tiny_num_small(TinyArgs a, TinyFused f) {
+    int k = 0;
+    while (k + 1 < f.nclass && (int)blockIdx.x >= f.blk0[k + 1]) ++k;
+    const int bid = (int)blockIdx.x - f.blk0[k], nb = f.blk0[k + 1] - f.blk0[k];
+    a.count = f.count[k];
+    a.bin = NUM_TINY + f.c[k];
+    a.list += (long long)(a.bin - 1) * a.M;
+    switch (f.c[k]) {
+    case 0: tiny_rows<8, 1, true>(a, bid, nb); break;
+    case 1: tiny_rows<32, 1, true>(a, bid, nb); break;
+    case 2: tiny_rows<32, 2, true>(a, bid, nb); break;
+    default: tiny_rows<32, 4, true>(a, bid, nb); break;
+    }
+}
+
 // Every symbolic tiny class in one launch (the bins' sizes are on the device): blocks
 // [TINY_SYM_GRID*c, TINY_SYM_GRID*(c+1)) walk class c's list.
 constexpr int TINY_SYM_GRID = 1024;
@@ -2747,24 +2770,42 @@ void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, i
         hipLaunchKernelGGL(k_num_wave_direct<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
                            WPB * NUM_W16_BYTES, s, a);
     }
-    for (int c = TINY_NC - 1; c >= 0; --c) {
-        const int count = h.num_count[NUM_TINY + c];
-        if (count <= 0) continue;
+    {
         TinyArgs t{};
         t.M = A.M;
-        t.count = count;
-        t.bin = NUM_TINY + c;
         t.Aptr = A.ptr;
         t.Acol = A.col;
         t.Aval = A.val;
         t.bmeta = w.bmeta;
         t.Bcol = B.col;
         t.Bval = B.val;
-        t.list = w.bin_list + (long long)(t.bin - 1) * A.M;
         t.Cptr = Cptr;
         t.Ccol = Ccol;
         t.Cval = Cval;
-        launch_tiny_num(c, count, t, s);
+        for (int c = TINY_NC - 1; c >= 4; --c) {  // 64-lane classes: kernels of their own (registers)
+            const int count = h.num_count[NUM_TINY + c];
+            if (count <= 0) continue;
+            TinyArgs tc = t;
+            tc.count = count;
+            tc.bin = NUM_TINY + c;
+            tc.list = w.bin_list + (long long)(tc.bin - 1) * A.M;
+            launch_tiny_num(c, count, tc, s);
+        }
+        TinyFused f{};
+        static_assert(tiny_w(3) == 32 && tiny_k(3) == 4 && tiny_w(4) == 64, "classes 0..3 fuse (W <= 32, K <= 4)");
+        for (int c = 3; c >= 0; --c) {
+            const int count = h.num_count[NUM_TINY + c];
+            if (count <= 0) continue;
+            const int per = 256 / tiny_w(c);
+            f.c[f.nclass] = c;
+            f.count[f.nclass] = count;
+            f.blk0[f.nclass + 1] = f.blk0[f.nclass] + round8((count + per - 1) / per, 4096);
+            ++f.nclass;
+        }
+        if (f.nclass > 0) {
+            t.list = w.bin_list;
+            hipLaunchKernelGGL(k_tiny_num_small, dim3(f.blk0[f.nclass]), dim3(256), 256 * 4 * 8, s, t, f);
+        }
     }
     if (h.num_count[NUM_W16G] > 0) {
         const int count = a.count = h.num_count[NUM_W16G];
