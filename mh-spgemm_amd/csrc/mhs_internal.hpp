@@ -163,8 +163,8 @@ __host__ __device__ inline bool sym_direct(int span, int tflop) {
 }
 __host__ __device__ inline long long sym_need(int span, int tflop) {
     int bound = tflop < span ? tflop : span;
-    int e = sym_direct(span, tflop) ? span : hash_slots(bound);
-    return (long long)e * 16;
+    // symbolic tables: masks (8 B a slot), plus keys (4 B) when hashed -- see sym_row
+    return sym_direct(span, tflop) ? align16((long long)span * 8) : align16((long long)hash_slots(bound) * 12);
 }
 // Numeric row modes:
 //   NM_DENSE  narrow tile span: a dense accumulator over the span's columns

@@ -1411,6 +1411,38 @@ struct SymArgs {
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
 };
 
+// Symbolic tile table (counts only, no ranks): masks Mk[H], then -- hashed -- keys Kk[H]:
+// 8 or 12 bytes a slot (sym_need), so more rows fit the small-table wave bin.
+struct SymTileBuild {
+    static constexpr bool kValues = false;
+    unsigned long long* Mk;
+    int* Kk;
+    bool direct;
+    int lo, H;
+    const int* __restrict__ btcol;
+    const unsigned long long* __restrict__ btmask;
+    struct Item {
+        int tc;
+        unsigned long long m;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{btcol[i], btmask[i]}; }
+    __device__ __forceinline__ void put(const Item& x, double) const {
+        if (direct) {
+            atomicOr(&Mk[x.tc - lo], x.m);
+        } else {
+            int s = hslot(x.tc, H);
+            for (;;) {
+                const int old = atomicCAS(&Kk[s], -1, x.tc);
+                if (old == -1 || old == x.tc) {
+                    atomicOr(&Mk[s], x.m);
+                    break;
+                }
+                s = hnext(s, H);
+            }
+        }
+    }
+};
+
 template <class Team>
 __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E, int4* stage) {
     const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
@@ -1419,16 +1451,21 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
     const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
     const bool direct = sym_direct(span, tflop);
     const int H = direct ? span : hash_slots(tflop < span ? tflop : span);
-    clear_tiles(tm, E, H);
+    unsigned long long* Mk = reinterpret_cast<unsigned long long*>(E);
+    int* Kk = reinterpret_cast<int*>(Mk + H);
+    for (int s = tm.rank(); s < H; s += Team::size) {
+        Mk[s] = 0ull;
+        if (!direct) Kk[s] = -1;
+    }
     tm.sync();
-    build_tiles(tm, E, direct, lo, H, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
-                __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]), a.Acol, a.bmeta, a.btcol, a.btmask,
-                tflop, stage);
+    walk_products(tm, __builtin_amdgcn_readfirstlane(a.Aptr[row]), __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]),
+                  a.Acol, nullptr, a.bmeta, true, tflop, SymTileBuild{Mk, Kk, direct, lo, H, a.btcol, a.btmask},
+                  stage);
     tm.sync();
     long long n = 0;
     int t = 0;
     for (int s = tm.rank(); s < H; s += Team::size) {
-        const unsigned long long m = E[s].mask;
+        const unsigned long long m = Mk[s];
         n += __popcll(m);
         t += m != 0;
     }
@@ -1442,7 +1479,7 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
     // numeric reuses the OR'd masks of narrow rows (span <= 32 < team size: one store per lane)
     const int r_ = tm.rank();
     if (direct && span <= MCACHE_SPAN && r_ < span && a.mcache) {
-        const unsigned long long m = E[r_].mask;
+        const unsigned long long m = Mk[r_];
         for (int g = 0; g < R; ++g) a.mcache[(size_t)(row + g) * a.mc_stride + r_] = m;
     }
     // ... and the compacted (key, mask) list of the other rows with few tiles
@@ -1451,16 +1488,15 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
         int k = 0;
         for (int s0 = 0; s0 < H; s0 += 64) {
             const int sl = s0 + lane;
-            uint4 q = make_uint4(0, 0, 0, 0);
-            if (sl < H) q = *reinterpret_cast<const uint4*>(&E[sl]);  // mask, base, key
-            const bool occ = (q.x | q.y) != 0u;
+            const unsigned long long m = sl < H ? Mk[sl] : 0ull;
+            const bool occ = m != 0ull;
             const unsigned long long bal = __ballot(occ);
             if (occ) {
                 const int pos = k + __popcll(bal & lanemask_lt());
-                const int key = direct ? lo + sl : (int)q.w;
+                const int key = direct ? lo + sl : Kk[sl];
                 for (int g = 0; g < R; ++g) {
                     unsigned long long* slot = a.mcache + (size_t)(row + g) * a.mc_stride;
-                    slot[pos] = ((unsigned long long)q.y << 32) | q.x;
+                    slot[pos] = m;
                     reinterpret_cast<int*>(slot + a.mc_list)[pos] = key;
                 }
             }
