@@ -2147,12 +2147,13 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                         mk &= mk - 1;
                     }
                 }
-                while (bigs) {
+                while (bigs) {  // the tile's entry re-read by every lane (a broadcast LDS read)
                     const int src = __builtin_ctzll(bigs);
                     bigs &= bigs - 1;
-                    const unsigned long long m2 = __shfl(mk, src);
-                    const int k2 = __shfl(key, src), b2 = __shfl(base, src);
-                    if ((m2 >> lane) & 1ull) cb[b2 + __popcll(m2 & lanemask_lt())] = (k2 << TILE_SHIFT) + lane;
+                    const uint4 q = *reinterpret_cast<const uint4*>(&E[s0 + src]);  // mask, base, key
+                    const unsigned long long m2 = ((unsigned long long)q.y << 32) | q.x;
+                    const int k2 = MODE != NM_HASH ? lo + s0 + src : (int)q.w;
+                    if ((m2 >> lane) & 1ull) cb[(int)q.z + __popcll(m2 & lanemask_lt())] = (k2 << TILE_SHIFT) + lane;
                 }
             }
             tm.sync();
