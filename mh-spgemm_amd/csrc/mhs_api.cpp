@@ -45,6 +45,7 @@ struct mhs_ctx {
     std::vector<hipEvent_t> nev;
     long long ncalls = 0;
     int mc_list = 0;         // tile-list cap of the row cache (0: mc_list_for(M); MHS_MC_LIST)
+    bool stats_zero = false; // the workspace's device Stats are zero (left so by the last k_scan)
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays)
@@ -309,8 +310,10 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // ---- mem_alloc: workspace (cached across calls) + C.ptr --------------------
     const int mc_list = ctx->mc_list > 0 ? ctx->mc_list : mc_list_for(M);
     const Layout L = plan(M, MB, A->nnz, B->nnz, mc_list);
+    const char* ws_before = ctx->ws;
     int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
     if (rc) return rc;
+    if (ctx->ws != ws_before) ctx->stats_zero = false;
     MHS_HIP(pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4));
     Work w{};
     w.btcol = (int*)(ctx->ws + L.btcol);
@@ -336,7 +339,9 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     w.stats = (Stats*)(ctx->ws + L.stats);
     w.gscratch = ctx->gscratch;
     w.gscratch_bytes = ctx->gscratch_bytes;
-    MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
+    // device Stats start zeroed: the previous call's k_scan left them so, else a memset
+    if (!ctx->stats_zero) MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
+    ctx->stats_zero = false;  // until this call's k_scan has published and cleared them
     if (M == 0) {
         MHS_HIP(hipMemsetAsync(out.ptr, 0, 4, s));
     }
@@ -373,6 +378,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
             return rc;
         }
         memcpy(&h, (const void*)&ctx->pub->stats, sizeof(Stats));
+        ctx->stats_zero = true;  // k_scan's last block cleared them after publishing
     } else {
         MHS_HIP(hipGetLastError());
         MHS_HIP(hipMemcpyAsync(ctx->h_stats, w.stats, sizeof(Stats), hipMemcpyDeviceToHost, s));

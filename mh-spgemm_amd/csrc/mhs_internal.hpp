@@ -82,7 +82,10 @@ constexpr int SYM_WAVE_WORK = 4096;     // tile products a single wave takes on
 constexpr int SYM_WM_BYTES = (LDS_MAX_C - 1024) / 16;  // 16 waves of a 1024-thread block (k_sym_rare): 16 waves per CU
 constexpr int SYM_B256_BYTES = 32768;
 constexpr int SYM_B256_WORK = 1 << 20;
-constexpr int NUM_WS_BYTES = 5120;   // 4 waves x 5 KiB = 20 KiB/block: 8 blocks (32 waves) per CU
+#ifndef MHS_NUM_WS_BYTES
+#define MHS_NUM_WS_BYTES 5120
+#endif
+constexpr int NUM_WS_BYTES = MHS_NUM_WS_BYTES;   // 4 waves x 5 KiB = 20 KiB/block: 8 blocks (32 waves) per CU
 constexpr int NUM_WS_WORK = 8192;       // products a single wave takes on
 constexpr int NUM_W16_BYTES = 16384;
 constexpr int NUM_W16_WORK = 32768;

@@ -1869,7 +1869,13 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         }
         __syncthreads();
     }
-    if (pub) publish_stats(stats, pub, seq);
+    if (pub) {
+        publish_stats(stats, pub, seq);
+        // the host has its copy: leave the device Stats zeroed for the next call (nothing
+        // after this kernel reads them), which saves that call a memset launch
+        __syncthreads();
+        if (threadIdx.x < (int)(sizeof(Stats) / 4)) reinterpret_cast<int*>(stats)[threadIdx.x] = 0;
+    }
 }
 
 // --------------------------------------------------------------- numeric ---
