@@ -1783,6 +1783,15 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     if (threadIdx.x == 0 && bid > 0)
         __hip_atomic_store(&state[bid], LB_AGG | (unsigned long long)total, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+    {  // total products: every block adds its share of k_analyze's per-block partials
+       // (off the tail: the last block only publishes)
+        const int per = (nflop + (int)gridDim.x - 1) / (int)gridDim.x;
+        const int i1 = min(nflop, (bid + 1) * per);
+        unsigned long long f = 0;
+        for (int i = bid * per + threadIdx.x; i < i1; i += 1024) f += blkflop[i];
+        f = wave_sum(f);
+        if (lane == 0 && f) atomicAdd(&stats->flop, f);
+    }
     // numeric bin of every row (independent of the prefix: its loads overlap the
     // predecessors' publication instead of following the look-back)
     __shared__ unsigned char nbin_of[SCAN_ITEMS];
@@ -1859,20 +1868,6 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     __syncthreads();
     append_block_rows<NUM_NB>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
-    {  // total products = sum of k_analyze's per-block partials
-        __shared__ unsigned long long fs[16];
-        unsigned long long f = 0;
-        for (int i = threadIdx.x; i < nflop; i += 1024) f += blkflop[i];
-        f = wave_sum(f);
-        if (lane == 0) fs[w] = f;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long t = 0;
-            for (int k = 0; k < 16; ++k) t += fs[k];
-            stats->flop = t;
-        }
-        __syncthreads();
-    }
     if (pub) {
         publish_stats(stats, pub, seq);
         // the host has its copy: leave the device Stats zeroed for the next call (nothing
