@@ -1736,11 +1736,13 @@ __device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t
 
 // Row pointer = exclusive scan of the C row nnz (items [0, M]; item M = 0 gives
 // row_ptr[M]) in ONE pass with decoupled look-back: blocks take tickets in dispatch
-// order, publish their aggregate, add up their predecessors' (inclusive prefix once
-// one is found) and publish their own inclusive prefix.  Every predecessor holds an
-// earlier ticket, so it has started and publishes without waiting on this block.  The
-// same pass gives every row its numeric bin and appends it to the bin lists; the last
-// block to finish totals the products and publishes Stats to the host.
+// order (big grids), publish their aggregate, add up their predecessors' (inclusive
+// prefix once one is found) and publish their own inclusive prefix.  Every predecessor
+// holds an earlier ticket, so it has started and publishes without waiting on this
+// block.  The same pass gives every row its numeric bin and appends it to the bin
+// lists, and every block adds its share of the product total; the last block to finish
+// publishes Stats to the host.
+constexpr int SCAN_TICKET_MIN = 256;  // k_scan grids above this take dispatch-order tickets
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
 __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                unsigned long long* __restrict__ state,
@@ -1759,9 +1761,15 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     __shared__ long long excl_s;
     __shared__ int bid_s;
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) bid_s = atomicAdd(&stats->scan_ticket, 1);
-    __syncthreads();
-    const int bid = bid_s;
+    // grids of <= 256 blocks (M <= 256K rows) are co-resident (a 1024-thread block with
+    // ~1 KiB of LDS fits any CU), so no block can wait on one that never starts: the
+    // block index serves, and the ticket's atomic round trip leaves the critical path
+    int bid = blockIdx.x;
+    if (gridDim.x > SCAN_TICKET_MIN) {
+        if (threadIdx.x == 0) bid_s = atomicAdd(&stats->scan_ticket, 1);
+        __syncthreads();
+        bid = bid_s;
+    }
     const int base = bid * SCAN_ITEMS + threadIdx.x * PER;
     int v[PER];
     long long loc = 0;
