@@ -1636,14 +1636,9 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
 // binof[j]) to contiguous per-bin lists: bin x's rows at list + (x-1)*M, cursor
 // cnt[x].  The block's rows keep row order; one atomic per (block, bin) reserves
 // their places (the grids that call this have M/4096 blocks: little contention).
-struct NoWaveWork {
-    __device__ void operator()() const {}
-};
-// wave0(): work of wave 0 while waves 1..NB-1 reserve the block's places (k_scan: the
-// look-back), finished before the list writes
-template <int NB, class W0 = NoWaveWork>
+template <int NB>
 __device__ void append_block_rows(const unsigned char* binof, long long M, int* __restrict__ cnt,
-                                  int* __restrict__ list, int blk, const W0& wave0 = W0{}) {
+                                  int* __restrict__ list, int blk) {
     constexpr int PER = SCAN_ITEMS / 1024;
     static_assert(PER * 16 <= 64 && NB <= 16, "one wave scans one bin's (pass, wave) counts");
     __shared__ int wc[NB][PER * 16];  // [bin][pass*16 + wave]: members, then exclusive prefix
@@ -1661,9 +1656,7 @@ __device__ void append_block_rows(const unsigned char* binof, long long M, int* 
         }
     }
     __syncthreads();
-    if (w == 0) {
-        wave0();
-    } else if (w < NB) {  // wave x: exclusive prefix over (pass, wave); reserve the block's places
+    if (w >= 1 && w < NB) {  // wave x: exclusive prefix over (pass, wave); reserve the block's places
         const int c = lane < PER * 16 ? wc[w][lane] : 0;
         const int inc = wave_incl_scan(c);
         if (lane < PER * 16) wc[w][lane] = inc - c;
@@ -1833,8 +1826,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
     }
     __syncthreads();
-    // wave 0 walks the look-back while waves 1.. reserve the block's list places
-    auto lookback = [&]() {
+    if (w == 0) {
         // wave 0 looks back over 64 predecessors per round trip: lane l reads block j - l;
         // the nearest inclusive prefix ends the walk, the aggregates above it are summed
         // (a window with an unpublished block before that point is re-read)
@@ -1872,8 +1864,8 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                 if (ex + total > INT_MAX) atomicOr(&stats->err, ERR_OVERFLOW);
             }
         }
-    };
-    append_block_rows<NUM_NB>(nbin_of, M, stats->num_count, list, bid, lookback);
+    }
+    __syncthreads();
     long long off = excl_s + woff + inc - loc;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -1881,6 +1873,8 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         if (i <= M) Cptr[i] = (int)off;
         off += v[k];
     }
+    __syncthreads();
+    append_block_rows<NUM_NB>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
     if (pub) {
         publish_stats(stats, pub, seq);
