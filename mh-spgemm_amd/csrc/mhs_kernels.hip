@@ -83,6 +83,9 @@
 #ifndef MHS_WPE_HASH
 #define MHS_WPE_HASH 8  // measured: cop20k-like numeric -18%, cage15-like -16% (vs the compiler's 6)
 #endif
+#ifndef MHS_WPE_GRP
+#define MHS_WPE_GRP 0  // occupancy floor of the generic / grouped wave numeric kernel (0: compiler's choice)
+#endif
 #ifndef MHS_WPE_DIRECT
 #define MHS_WPE_DIRECT 0
 #endif
@@ -2321,7 +2324,11 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
 }
 
 template <int BYTES, bool GROUPED = false, bool HASH = false>
+#if MHS_WPE_GRP > 0
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_GRP) void k_num_wave(NumArgs a) {
+#else
 __global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
+#endif
     num_wave_rows<BYTES, GROUPED, HASH>(a);
 }
 template <int BYTES>
