@@ -83,6 +83,9 @@
 #ifndef MHS_WPE_HASH
 #define MHS_WPE_HASH 8  // measured: cop20k-like numeric -18%, cage15-like -16% (vs the compiler's 6)
 #endif
+#ifndef MHS_SYM_B256_GRID
+#define MHS_SYM_B256_GRID 1024  // block cap of the persistent 256-thread symbolic bin launch
+#endif
 #ifndef MHS_WPE_GRP
 #define MHS_WPE_GRP 0  // occupancy floor of the generic / grouped wave numeric kernel (0: compiler's choice)
 #endif
@@ -2753,7 +2756,7 @@ void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, 
     SymArgs a = sym_args(A, w, M, N, Cptr);
     hipLaunchKernelGGL(k_sym_rare, dim3(256), dim3(1024), LDS_MAX - 1024, s, a);
     a.bin = SYM_B256;
-    hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, 1024)), dim3(256), SYM_B256_BYTES, s, a);
+    hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, MHS_SYM_B256_GRID)), dim3(256), SYM_B256_BYTES, s, a);
 }
 
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
