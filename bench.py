@@ -19,14 +19,23 @@ rows the block references; full: the north_star's allgatherv of every block)
 beside it).  Total work is fixed, so scaling is "strong".
 
 One JSON line on rank 0: value = 2*flop / (max over ranks of the time per step).
-  roofline: the dominant kernel (the numeric phase: k_num_wave for this
-            workload), achieved = algorithmic bytes per launch (BASELINE.md §2:
-            B_alg = 8(M+1) + 20 nnz(A) + 12 flop + 12 nnz(C)) / its average
-            duration from hipEvents recorded on the launch stream during the
-            timed steps (MHS_OPT_NUMERIC_EVENTS); traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per launch
-            from the committed PMC pass (profiles/), else null.
+  roofline: the dominant kernel = the numeric phase (every numeric bin launch of a
+            call: k_num_wave<10240,true> alone on this workload), timed with
+            hipEvents recorded on the launch stream during the timed steps
+            (MHS_OPT_NUMERIC_EVENTS).  achieved = COMPULSORY bytes of that phase
+            per call / its average duration: read A once (row_ptr, col, val; B
+            aliases A), read C's row_ptr, write C's col and val:
+                B_comp = 8 (M+1) + 12 nnz(A) [+ B's arrays when B != A] + 12 nnz(C)
+            traffic = measured HBM bytes of the same launches per call
+            (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, separate --pmc passes, committed
+            under profiles/ and keyed by matrix; null for a matrix never profiled).
+            The old B_alg (12 B per product, as if every B gather missed to HBM)
+            is kept only as the labelled "gather_equiv_GBps": it is not a bound.
   cpu_baseline: the oracle (CPU restatement, "port") on the same matrix, all
             host cores, median of repeats.
+  cold_call: one call on a fresh context (empty workspace and C pool: every
+            hipMalloc inside, as the reference's Tool::allocate + C cudaMalloc,
+            src/Tool.cu:4-45, src/main.cu:54-61) beside the pooled steady state.
 """
 from __future__ import annotations
 
@@ -45,27 +54,45 @@ for p in (str(ROOT), str(ROOT / "mh-spgemm_amd")):
 import numpy as np  # noqa: E402
 
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+# numeric bin id -> kernel (mhs_internal.hpp NumBin; include/mhspgemm.h num_bins)
+NUM_BIN_KERNELS = ["", "k_num_wave_direct<5120>", "k_num_wave_direct<16384>", "k_num_block<256>",
+                   "k_num_block<1024>", "k_num_block<1024,global>", "k_num_wave<10240,grouped>",
+                   "k_num_wave<16384,grouped>", "k_tiny_num_small(8x1)", "k_tiny_num_small(32x1)",
+                   "k_tiny_num_small(32x2)", "k_tiny_num_small(32x4)", "k_tiny_num<64,4>", "k_tiny_num<64,8>",
+                   "k_num_wave_hash<5120>", "k_num_wave_hash<16384>"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
 def b_alg(M, nnzA, flop, nnzC):
+    """Gather-equivalent bytes (12 B per product): a diagnostic, not a bound."""
     return 8 * (M + 1) + 20 * nnzA + 12 * flop + 12 * nnzC
 
 
-def pmc_traffic(kernel_prefix: str):
-    """Per-launch HBM bytes of the kernel from the committed rocprofv3 PMC
-    summary (FETCH_SIZE doubled per the gfx950 correction, + WRITE_SIZE)."""
+def b_comp(M, nnzA, nnzC, nnzB_extra=0, MB_extra=0):
+    """Compulsory bytes of C = A*B: A's arrays read once, C.ptr read, C.col/C.val
+    written (B's arrays too when B does not alias A)."""
+    return 8 * (M + 1) + 12 * nnzA + 12 * nnzC + 12 * nnzB_extra + 4 * MB_extra
+
+
+NUMERIC_PREFIXES = ("k_num_", "k_tiny_num")
+
+
+def pmc_traffic(matrix: str):
+    """Measured HBM bytes per call of the numeric launches of `matrix` from the
+    committed rocprofv3 PMC summary (FETCH_SIZE doubled per the gfx950 correction,
+    + WRITE_SIZE).  Returns (bytes, source, kernels) or (None, None, None)."""
     f = ROOT / "profiles" / "pmc_summary.json"
-    if not f.exists():
-        return None, None
     try:
         d = json.loads(f.read_text())
-        k = d.get("kernels", {}).get(kernel_prefix)
-        if not k:
-            return None, None
-        return float(k["hbm_bytes_per_launch"]), d.get("source")
+        m = d["matrices"][matrix]
+        ks = {k: v for k, v in m["kernels"].items()
+              if k.split("::")[-1].startswith(NUMERIC_PREFIXES)}
+        if not ks:
+            return None, None, None
+        tot = sum(v["hbm_bytes_per_call"] for v in ks.values())
+        return float(tot), f"{m['source']} (head {d.get('head', '?')})", sorted(ks)
     except Exception:
-        return None, None
+        return None, None, None
 
 
 def cpu_baseline(A, budget_s: float = 12.0):
@@ -162,6 +189,15 @@ def main():
             phases.append(t)
             C.release()
         nnzC = t.nnzC
+        # cold call: a fresh context, so the workspace and C come from hipMalloc inside
+        # the call (the pooled steps above reuse them)
+        cold_tool = mhspgemm.Tool(local)
+        cold_tool.set_stream(torch.cuda.current_stream(local).cuda_stream)
+        C, tc = mhspgemm.spgemm(cold_tool, A, A, timing=True)
+        C.release()
+        cold_tool.close()
+        cold = {"t_e2e_ms": round(tc.total_e2e, 4), "gflops": round(2.0 * flop / (tc.total_e2e * 1e-3) / 1e9, 2),
+                "mem_alloc_ms": round(tc.mem_alloc, 4), "Malloc_C_col_val_ms": round(tc.Malloc_C_col_val, 4)}
     else:
         from mhspgemm import distributed as D
         rf = D.row_flop(A.ptr, A.col, A.ptr)
@@ -226,26 +262,30 @@ def main():
             "matrix": args.matrix, "rows": A.M, "nnzA": A.nnz, "flop": flop, "nnzC": nnzC,
             "parallelism": "single GPU" if N_GPUS == 1 else
                            f"row-sharded x{N_GPUS}, {args.exchange} exchange of B's rows in every step, C distributed",
+            "memory": "steady-state steps reuse the context's workspace and pooled C buffers "
+                      "(no hipMalloc in a step); cold_call times a fresh context",
         },
-        "e2e_alg_GBps": round(balg / (ms_per_step * 1e-3) / 1e9, 1),
     }
     if N_GPUS == 1:
         avg_num = float(np.mean(numeric_ms))
-        achieved = balg / (avg_num * 1e-3) / 1e9
-        traffic, tsrc = pmc_traffic("k_num_wave")
+        bc = b_comp(A.M, A.nnz, nnzC)
+        achieved = bc / (avg_num * 1e-3) / 1e9
+        traffic, tsrc, tkern = pmc_traffic(args.matrix)
+        nk = [k for k, c in zip(NUM_BIN_KERNELS, phases[-1].num_bins) if c > 0 and k]
         out["roofline"] = {
-            "bound": "hbm", "kernel": "numeric phase (k_num_wave<10240,true>: row groups, on this workload)",
+            "bound": "hbm", "kernel": "numeric phase: " + ", ".join(nk),
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": traffic, "traffic_source": tsrc,
-            "alg_bytes_per_launch": balg, "avg_launch_ms": round(avg_num, 4),
-            # B_alg counts 12 B per product as if every B read came from HBM; with row
-            # groups / B-row runs and L2/MALL reuse the kernel moves far less: the
-            # measured HBM rate below is the one to compare with the 8 TB/s peak
+            "traffic": traffic, "traffic_source": tsrc, "traffic_kernels": tkern,
+            "bytes_per_launch": bc, "bytes_definition": "compulsory: 8(M+1) + 12 nnz(A) + 12 nnz(C)",
+            "avg_launch_ms": round(avg_num, 4),
             "hbm_measured_GBps": round(traffic / (avg_num * 1e-3) / 1e9, 1) if traffic else None,
             "frac_measured": round(traffic / (avg_num * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
-            "e2e_frac": round(balg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "e2e_frac": round(bc / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "gather_equiv_GBps": round(balg / (ms_per_step * 1e-3) / 1e9, 1),
         }
+        assert out["roofline"]["frac"] <= 1.0 and out["roofline"]["e2e_frac"] <= 1.0, out["roofline"]
+        out["cold_call"] = cold
         ph = {k: round(float(np.mean([getattr(p, k) for p in phases])), 4)
               for k in ("mem_alloc", "Form_mask_matrix_B", "symbolic_binning", "Calculate_C_nnz",
                         "numeric_binning", "Malloc_C_col_val", "Numeric", "total_e2e")}

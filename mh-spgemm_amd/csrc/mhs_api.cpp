@@ -48,9 +48,9 @@ struct mhs_ctx {
     bool stats_zero = false; // the workspace's device Stats are zero (left so by the last k_scan)
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
-    // output pool (caching allocator for C arrays)
+    // output pool (caching allocator for C arrays): (buffer, allocation size)
     std::vector<std::pair<void*, size_t>> pool;
-    std::unordered_map<void*, size_t> sizes;
+    hipEvent_t stream_ev = nullptr;  // orders a new caller stream after the previous one
 };
 
 namespace {
@@ -112,7 +112,6 @@ hipError_t pool_get(mhs_ctx* ctx, void** p, size_t bytes) {
     if (best != (size_t)-1) {
         *p = ctx->pool[bi].first;
         ctx->pool.erase(ctx->pool.begin() + (long)bi);
-        ctx->sizes[*p] = best;
         return hipSuccess;
     }
     hipError_t e = hipMalloc(p, bytes);
@@ -122,19 +121,22 @@ hipError_t pool_get(mhs_ctx* ctx, void** p, size_t bytes) {
         (void)hipGetLastError();
         e = hipMalloc(p, bytes);
     }
-    if (e == hipSuccess) ctx->sizes[*p] = bytes;
     return e;
 }
 
+// The buffer's true size comes from the runtime (not from a side table: a buffer
+// freed with mhs_csr_free and handed out again by hipMalloc at the same address
+// would otherwise be filed under its old size).
 void pool_put(mhs_ctx* ctx, void* p) {
     if (!p) return;
-    auto it = ctx->sizes.find(p);
-    if (it == ctx->sizes.end()) {
+    hipDeviceptr_t base = nullptr;
+    size_t bytes = 0;
+    if (hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t)p) != hipSuccess || base != (hipDeviceptr_t)p) {
+        (void)hipGetLastError();
         (void)hipFree(p);
         return;
     }
-    ctx->pool.emplace_back(p, it->second);
-    ctx->sizes.erase(it);
+    ctx->pool.emplace_back(p, bytes);
     // keep the pool bounded: drop the oldest buffers beyond 16 entries
     while (ctx->pool.size() > 16) {
         (void)hipFree(ctx->pool.front().first);
@@ -214,6 +216,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ctx->d_pub, ctx->pub, 0);
     if (e == hipSuccess) memset(ctx->pub, 0, sizeof(Published));
     for (int i = 0; e == hipSuccess && i < 8; ++i) e = hipEventCreate(&ctx->ev[i]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->stream_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = init_kernel_attributes();
     if (e != hipSuccess) {
         fprintf(stderr, "mhs_ctx_create: %s\n", hipGetErrorString(e));
@@ -233,8 +236,8 @@ void mhs_ctx_destroy(mhs_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    mhs_ctx_trim(ctx);
-    for (auto& kv : ctx->sizes) (void)kv;  // outstanding C buffers belong to the caller
+    mhs_ctx_trim(ctx);  // outstanding C buffers belong to the caller
+    if (ctx->stream_ev) (void)hipEventDestroy(ctx->stream_ev);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->pub) (void)hipHostFree(ctx->pub);
     for (auto& ev : ctx->nev)
@@ -249,7 +252,16 @@ const char* mhs_last_error(const mhs_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 int mhs_ctx_set_stream(mhs_ctx* ctx, void* s) {
     if (!ctx) return MHS_ERR_INVALID;
-    ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    hipStream_t next = s ? (hipStream_t)s : ctx->own_stream;
+    if (next != ctx->stream) {
+        // the workspace is shared by every call: work queued on the old stream (an
+        // unsynchronised call's numeric phase) must finish before the new stream's
+        // first kernel rewrites it
+        MHS_HIP(hipSetDevice(ctx->device));
+        MHS_HIP(hipEventRecord(ctx->stream_ev, ctx->stream));
+        MHS_HIP(hipStreamWaitEvent(next, ctx->stream_ev, 0));
+        ctx->stream = next;
+    }
     return MHS_OK;
 }
 

@@ -609,6 +609,7 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
     long long flop = 0, tflop = 0;
     int lo = INT_MAX, hi = -1;
     bool differ = true;  // row's column pattern differs from row-1's (row groups)
+    bool bad = false;    // an A column outside [0, B.M): the row is never walked (MHS_ERR_INVALID)
     if (valid) {
         const int s = Aptr[row], e = Aptr[row + 1];
         const int ps = row > 0 ? Aptr[row - 1] : 0;
@@ -621,6 +622,7 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
             differ = differ || kp != k;
             if (k < 0 || k >= MB) {
                 err = ERR_ACOL_RANGE;
+                bad = true;
                 continue;
             }
             const int4 m = bmeta[k];
@@ -638,10 +640,14 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         hi = max(hi, __shfl_xor(hi, d));
         const int od = __shfl_xor((int)differ, d);  // every lane shuffles (no short circuit)
         differ = differ || od != 0;
+        const int ob = __shfl_xor((int)bad, d);
+        bad = bad || ob != 0;
     }
     if (valid && gl == 0) {
-        asame[row] = (unsigned char)(differ ? 0 : 1);
-        const int f = sat_int(flop), tf = sat_int(tflop);
+        // a row with an out-of-range column enters no bin: the symbolic kernels gather
+        // bmeta[Acol[j]] unchecked, and the host returns MHS_ERR_INVALID before numeric
+        asame[row] = (unsigned char)((differ || bad) ? 0 : 1);
+        const int f = bad ? 0 : sat_int(flop), tf = bad ? 0 : sat_int(tflop);
         const int span = f ? hi - lo + 1 : 0;
         rflop[row] = f;
         rtflop[row] = tf;

@@ -184,6 +184,137 @@ def cage15_like(seed: int = 7) -> CSR:
     return banded_random(5_154_859, 18.2, 300, far_frac=0.10, seed=seed)
 
 
+# ---- headline robustness variants ---------------------------
+
+def cant_s1(seed: int = 2) -> CSR:
+    """SURVEY §8(d) S1 exactly as specified: n = 62,451, every row 64 entries as 4
+    runs of 16 consecutive columns placed at random within +-1,500 of the diagonal,
+    then symmetrised (pattern of A + A^T; the mirrored entry takes the row's value
+    where both exist).  No dof structure: rows do not repeat their neighbours'
+    patterns, so the row-group path does not fire."""
+    rng = np.random.default_rng(seed)
+    n = 62_451
+    starts = np.arange(n)[:, None] + rng.integers(-1500, 1500 - 16 + 1, size=(n, 4))
+    starts = np.clip(starts, 0, n - 16)
+    cols = (starts[:, :, None] + np.arange(16)[None, None, :]).reshape(n, 64)
+    rows = np.repeat(np.arange(n, dtype=np.int64), 64)
+    cols = cols.reshape(-1).astype(np.int64)
+    r = np.concatenate([rows, cols])
+    c = np.concatenate([cols, rows])
+    return _csr_from_coo(n, n, r, c, rng)
+
+
+def cant_perturbed(seed: int = 2, drop: float = 0.03) -> CSR:
+    """cant-like (27-point x 3-dof FEM grid) with `drop` of its off-diagonal entries
+    removed at random (not symmetrically): dof runs and row groups break where an
+    entry is missing, as boundary conditions and pruned entries do in the real cant."""
+    A = cant_like(seed)
+    rng = np.random.default_rng(seed + 1000)
+    rows = np.repeat(np.arange(A.M, dtype=np.int64), np.diff(A.ptr))
+    keep = (rows == A.col) | (rng.random(A.nnz) >= drop)
+    ptr = np.zeros(A.M + 1, np.int64)
+    np.cumsum(np.bincount(rows[keep], minlength=A.M), out=ptr[1:])
+    return CSR(A.M, A.N, ptr.astype(np.int32), A.col[keep], A.val[keep])
+
+
+# ---- stand-ins for the rest of 16matrix.txt (reference 16matrix.txt:1-16) --------
+
+def fem_stencil(dims, dof: int, stencil: str = "27", seed: int = 2) -> CSR:
+    """Node stencil on a 2-D or 3-D grid (`stencil` "27": every neighbour incl.
+    diagonals -- 9 in 2-D; "7": face neighbours -- 5 in 2-D), `dof` unknowns per node."""
+    if len(dims) == 2:
+        dims = (dims[0], dims[1], 1)
+    nx, ny, nz = dims
+    if stencil == "27":
+        offs = [(dx, dy, dz) for dx in (-1, 0, 1) for dy in (-1, 0, 1) for dz in (-1, 0, 1)]
+    else:
+        offs = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
+    offs = [o for o in offs if nz > 1 or o[2] == 0]
+    rng = np.random.default_rng(seed)
+    x, y, z = np.meshgrid(np.arange(nx), np.arange(ny), np.arange(nz), indexing="ij")
+    x, y, z = x.ravel(), y.ravel(), z.ravel()
+    node = x + nx * (y + ny * z)
+    rs, cs = [], []
+    for dx, dy, dz in offs:
+        xx, yy, zz = x + dx, y + dy, z + dz
+        ok = (xx >= 0) & (xx < nx) & (yy >= 0) & (yy < ny) & (zz >= 0) & (zz < nz)
+        a, b = node[ok], (xx + nx * (yy + ny * zz))[ok]
+        for d in range(dof):
+            for e in range(dof):
+                rs.append(dof * a + d)
+                cs.append(dof * b + e)
+    n = nx * ny * nz * dof
+    return _csr_from_coo(n, n, np.concatenate(rs), np.concatenate(cs), rng)
+
+
+def _tiled_order(side_x: int, side_y: int, tile: int = 32) -> np.ndarray:
+    """Node numbering of a side_x x side_y grid by tile x tile blocks (row-major
+    blocks, row-major inside): graph neighbours stay within a few thousand ids."""
+    x, y = np.meshgrid(np.arange(side_x), np.arange(side_y), indexing="xy")
+    x, y = x.ravel(), y.ravel()
+    tx, ty = x // tile, y // tile
+    ntx = (side_x + tile - 1) // tile
+    key = ((ty * ntx + tx) * tile + (y % tile)) * tile + (x % tile)
+    order = np.empty(len(key), np.int64)
+    order[np.argsort(key, kind="stable")] = np.arange(len(key))
+    return order.reshape(side_y, side_x)
+
+
+def road_like(n: int = 23_947_347, p: float = 0.6, seed: int = 8) -> CSR:
+    """GAP-road-like: a planar road network of ~2.4 entries per row, symmetric, no
+    diagonal: the edges of a grid (right and down neighbours, each kept with
+    probability p: mean degree 4p) on tiled node ids."""
+    rng = np.random.default_rng(seed)
+    side = int(np.ceil(np.sqrt(n)))
+    ids = _tiled_order(side, side)
+    rs, cs = [], []
+    for dx, dy in ((1, 0), (0, 1)):
+        a = ids[: side - dy, : side - dx].ravel()
+        b = ids[dy:, dx:].ravel()
+        keep = (rng.random(len(a)) < p) & (a < n) & (b < n)
+        rs += [a[keep], b[keep]]
+        cs += [b[keep], a[keep]]
+    return _csr_from_coo(n, n, np.concatenate(rs), np.concatenate(cs), rng)
+
+
+def delaunay_like(side: int = 4096, seed: int = 9) -> CSR:
+    """delaunay_n24-like (2^24 points, ~6 entries per row, no diagonal): a grid
+    triangulated with a random diagonal per cell (mean degree 6, varying), tiled ids."""
+    rng = np.random.default_rng(seed)
+    n = side * side
+    ids = _tiled_order(side, side)
+    rs, cs = [], []
+    for dx, dy in ((1, 0), (0, 1)):
+        a, b = ids[: side - dy, : side - dx].ravel(), ids[dy:, dx:].ravel()
+        rs += [a, b]
+        cs += [b, a]
+    flip = rng.random((side - 1, side - 1)) < 0.5
+    a = np.where(flip, ids[:-1, :-1], ids[:-1, 1:]).ravel()   # (x,y)-(x+1,y+1) or (x+1,y)-(x,y+1)
+    b = np.where(flip, ids[1:, 1:], ids[1:, :-1]).ravel()
+    rs += [a, b]
+    cs += [b, a]
+    return _csr_from_coo(n, n, np.concatenate(rs), np.concatenate(cs), rng)
+
+
+def wb_edu_like(seed: int = 10) -> CSR:
+    """wb-edu-like: 9,845,725 rows of a power-law web crawl, ~5.8 entries per row,
+    mostly site-local links plus Zipf-popular hubs."""
+    return powerlaw(9_845_725, alpha=2.12, cap=4700, local_frac=0.8, local_width=2048, zipf_s=1.2, seed=seed)
+
+
+def offshore_like(seed: int = 11) -> CSR:
+    """offshore-like: 3-D 7-point stencil x 2 dof (~14/row) on 64 x 64 x 32 nodes plus
+    a few random local couplings (~16/row): n = 262,144 (real 259,789)."""
+    A = fem_stencil((64, 64, 32), 2, "7", seed=seed)
+    rng = np.random.default_rng(seed)
+    rows = np.repeat(np.arange(A.M, dtype=np.int64), np.diff(A.ptr))
+    extra = rng.integers(0, A.M, A.M)
+    er = (extra + rng.integers(-3000, 3001, A.M)) % A.M
+    r = np.concatenate([rows, extra, er])
+    c = np.concatenate([A.col.astype(np.int64), er, extra])
+    return _csr_from_coo(A.M, A.N, r, c, rng)
+
+
 SYNTH = {
     "cage4": cage4_like,
     "cant": cant_like,
@@ -192,7 +323,25 @@ SYNTH = {
     "scircuit": scircuit_like,
     "cop20k_A": cop20k_like,
     "cage15": cage15_like,
+    # headline robustness variants
+    "cant-s1": cant_s1,
+    "cant-perturbed": cant_perturbed,
+    # the rest of 16matrix.txt
+    "pdb1HYS": lambda: fem_stencil((11, 11, 75), 4, "27", seed=12),     # n 36,300 (real 36,417), ~100/row
+    "pwtk": lambda: fem_stencil((31, 31, 113), 2, "27", seed=13),       # n 217,186 (real 217,918), ~50/row
+    "cage12": lambda: banded_random(130_228, 14.6, 300, far_frac=0.10, seed=14),  # ~15.6/row
+    "hood": lambda: fem_stencil((10, 10, 1103), 2, "27", seed=15),      # n 220,600 (real 220,542), ~45/row
+    "rma10": lambda: fem_stencil((88, 88), 6, "27", seed=16),           # 2-D, n 46,464 (real 46,835), ~52/row
+    "shipsec1": lambda: fem_stencil((40, 40, 44), 2, "27", seed=17),    # n 140,800 (real 140,874), ~50/row
+    "offshore": offshore_like,
+    "wb-edu": wb_edu_like,
+    "GAP-road": road_like,
+    "delaunay_n24": delaunay_like,
 }
+
+# reference 16matrix.txt, in its order (process.sh:21-37 walks it)
+MATRIX16 = ["pdb1HYS", "pwtk", "webbase-1M", "cage12", "cant", "hood", "rma10", "scircuit", "shipsec1",
+            "cop20k_A", "mac_econ_fwd500", "offshore", "wb-edu", "cage15", "GAP-road", "delaunay_n24"]
 
 
 def matrix_path(name: str) -> Path | None:
@@ -201,6 +350,25 @@ def matrix_path(name: str) -> Path | None:
         return None
     p = Path(root) / name / f"{name}.mtx"
     return p if p.exists() else None
+
+
+def _cached(name: str) -> CSR:
+    """SYNTH[name](), memoised as .npz under $MHS_SYNTH_CACHE when that is set
+    (the big stand-ins take tens of seconds to generate; several processes of one
+    GPU job then build them once)."""
+    root = os.environ.get("MHS_SYNTH_CACHE")
+    if not root:
+        return SYNTH[name]()
+    f = Path(root) / f"{name}.npz"
+    if f.exists():
+        d = np.load(f)
+        return CSR(int(d["M"]), int(d["N"]), d["ptr"], d["col"], d["val"])
+    A = SYNTH[name]()
+    f.parent.mkdir(parents=True, exist_ok=True)
+    tmp = f.with_suffix(f".{os.getpid()}.npz")
+    np.savez(tmp, M=A.M, N=A.N, ptr=A.ptr, col=A.col, val=A.val)
+    os.replace(tmp, f)
+    return A
 
 
 def load_or_synth(name: str) -> tuple[CSR, str]:
@@ -213,4 +381,4 @@ def load_or_synth(name: str) -> tuple[CSR, str]:
             return A, f"file:{p}"
     if name not in SYNTH:
         raise KeyError(f"no synthetic stand-in for {name!r}")
-    return SYNTH[name](), f"synthetic:{name}-like"
+    return _cached(name), f"synthetic:{name}-like"

@@ -223,6 +223,29 @@ def test_error_column_out_of_range(tool):
         mhspgemm.spgemm(tool, A, A)
 
 
+@pytest.mark.parametrize("long_row", [False, True])
+def test_error_column_out_of_range_mixed_row(tool, long_row):
+    # a row mixing valid and out-of-range columns: the row must enter no
+    # symbolic bin (its kernels gather bmeta[Acol[j]] unchecked) and the call must
+    # return MHS_ERR_INVALID; the context stays usable afterwards
+    if long_row:
+        Bp, Bc, Bv = random_csr(50, 3000, 100, seed=21)
+        cols = list(range(0, 40)) + [77]  # 40 valid B rows (~4000 products: a wave bin) + 1 bad
+        Ap = np.array([0, len(cols), len(cols) + 2], np.int32)
+        Ac = np.array(cols + [1, 2], np.int32)
+        A = mhspgemm.CSR(2, 50, Ap, Ac, np.ones(len(Ac)))
+        B = mhspgemm.CSR(50, 3000, Bp, Bc, Bv)
+    else:
+        A = mhspgemm.CSR(2, 2, np.array([0, 2, 2], np.int32), np.array([0, 5], np.int32), np.ones(2))
+        B = mhspgemm.CSR(2, 2, np.array([0, 1, 2], np.int32), np.array([0, 1], np.int32), np.ones(2))
+    A.H2D(tool.device)
+    B.H2D(tool.device)
+    with pytest.raises(mhspgemm.MHSpGEMMError) as e:
+        mhspgemm.spgemm(tool, A, B)
+    assert e.value.status == 3 and "A column" in str(e.value)
+    check(tool, synth.cage4_like(), synth.cage4_like())
+
+
 def test_repeat_calls_reuse_workspace(tool):
     A = synth.cage4_like()
     A.H2D(tool.device)
