@@ -275,10 +275,25 @@ def test_mirror_interface_MH_spgemm(tool):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("name", ["webbase-1M", "mac_econ_fwd500", "scircuit", "cop20k_A"])
+@pytest.mark.parametrize("name", ["webbase-1M", "mac_econ_fwd500", "scircuit", "cop20k_A",
+                                  # the headline's robustness variants (broken dof runs)
+                                  "cant-s1", "cant-perturbed",
+                                  # the rest of 16matrix.txt (stand-ins, synth.py)
+                                  "pdb1HYS", "pwtk", "cage12", "hood", "rma10", "shipsec1", "offshore"])
 def test_baseline_configs_full(tool, name):
     A = synth.SYNTH[name]()
     check(tool, A, A)
+    A.d_release_csr()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["wb-edu", "GAP-road", "delaunay_n24"])
+def test_huge_m_full(tool, name):
+    """16matrix.txt's huge-M, few-entries-per-row stand-ins (9.8 M - 24 M rows), whole
+    matrix against the oracle: row_ptr / col_idx bit-exact, values within 1e-6."""
+    A = synth.SYNTH[name]()
+    check(tool, A, A, ref_rule=False)
+    A.d_release_csr()
 
 
 @pytest.mark.slow
