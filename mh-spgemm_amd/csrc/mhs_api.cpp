@@ -47,10 +47,17 @@ struct mhs_ctx {
     int mc_list = 0;         // tile-list cap of the row cache (0: mc_list_for(M); MHS_MC_LIST)
     bool stats_zero = false; // the workspace's device Stats are zero (left so by the last k_scan)
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
+    bool tiny_num = true;    // numeric tiny (sort) classes (MHS_NO_TINY_NUM=1: off)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays): (buffer, allocation size)
     std::vector<std::pair<void*, size_t>> pool;
     hipEvent_t stream_ev = nullptr;  // orders a new caller stream after the previous one
+    // numeric bins on several streams (MHS_NUM_STREAMS, default 4; 1 = one stream): aux
+    // streams fork from the call's stream after the Stats hand-off and join it before return
+    static constexpr int NAUX = 7;
+    int num_streams = 4;
+    hipStream_t aux[NAUX] = {};
+    hipEvent_t fork_ev = nullptr, join_ev[NAUX] = {};
 };
 
 namespace {
@@ -217,6 +224,12 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (e == hipSuccess) memset(ctx->pub, 0, sizeof(Published));
     for (int i = 0; e == hipSuccess && i < 8; ++i) e = hipEventCreate(&ctx->ev[i]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->stream_ev, hipEventDisableTiming);
+    if (const char* v = getenv("MHS_NUM_STREAMS")) ctx->num_streams = std::max(1, std::min(atoi(v), mhs_ctx::NAUX + 1));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming);
+    for (int i = 0; e == hipSuccess && i + 1 < ctx->num_streams; ++i) {
+        e = hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming);
+    }
     if (e == hipSuccess) e = init_kernel_attributes();
     if (e != hipSuccess) {
         fprintf(stderr, "mhs_ctx_create: %s\n", hipGetErrorString(e));
@@ -228,6 +241,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (getenv("MHS_NO_MCACHE")) ctx->use_mcache = false;
     if (const char* e = getenv("MHS_MC_LIST")) ctx->mc_list = atoi(e) < MC_LIST_MIN ? MC_LIST_MIN : atoi(e);
     if (getenv("MHS_NO_GROUPS")) ctx->groups = false;
+    if (getenv("MHS_NO_TINY_NUM")) ctx->tiny_num = false;
     *out = ctx;
     return MHS_OK;
 }
@@ -238,6 +252,14 @@ void mhs_ctx_destroy(mhs_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     mhs_ctx_trim(ctx);  // outstanding C buffers belong to the caller
     if (ctx->stream_ev) (void)hipEventDestroy(ctx->stream_ev);
+    if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
+    for (int i = 0; i < mhs_ctx::NAUX; ++i) {
+        if (ctx->aux[i]) {
+            (void)hipStreamSynchronize(ctx->aux[i]);
+            (void)hipStreamDestroy(ctx->aux[i]);
+        }
+        if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
+    }
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->pub) (void)hipHostFree(ctx->pub);
     for (auto& ev : ctx->nev)
@@ -341,7 +363,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     w.asame = (unsigned char*)(ctx->ws + L.asame);
     w.grp = (unsigned char*)(ctx->ws + L.grp);
     w.groups = ctx->groups ? 1 : 0;
-    w.tiny_num = B->N <= TINY_NUM_NMAX ? 1 : 0;  // packed tiny sort keys hold the column in 23 bits
+    w.tiny_num = ctx->tiny_num ? 1 : 0;  // per row: packed sort keys hold its column offsets in 23 bits
     w.bin_list = (int*)(ctx->ws + L.bin_list);
     w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
     w.nflop = M > 0 ? analyze_blocks(A->nnz, M) : 0;
@@ -438,8 +460,28 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     const int nring = (int)ctx->nev.size() / 2;
     const int slot = nring ? (int)(ctx->ncalls % nring) : 0;
     if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
-    if (out.nnz > 0)
-        launch_numeric(a, b, w, h, out.ptr, out.col, out.val, s, NUM_GLOBAL_GRID, ctx->dense_span_max);
+    if (out.nnz > 0) {
+        // several heavy bins: deal them over the aux streams (fork/join costs ~10-20 us,
+        // so only when there are at least 3 launches of a product worth it)
+        hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
+        const int nl = numeric_launches(h);
+        int nss = (nl >= 3 && h.flop >= (1ull << 24)) ? std::min(ctx->num_streams, nl) : 1;
+        if (nss > 1) {
+            MHS_HIP(hipEventRecord(ctx->fork_ev, s));
+            for (int i = 1; i < nss; ++i) {
+                ss[i] = ctx->aux[i - 1];
+                MHS_HIP(hipStreamWaitEvent(ss[i], ctx->fork_ev, 0));
+            }
+        }
+        const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
+                                        ctx->dense_span_max);
+        MHS_HIP(hipGetLastError());
+        for (int i = 1; i < nss; ++i)
+            if (used & (1 << i)) {
+                MHS_HIP(hipEventRecord(ctx->join_ev[i - 1], ss[i]));
+                MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[i - 1], 0));
+            }
+    }
     MHS_HIP(hipGetLastError());
     if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
     ++ctx->ncalls;

@@ -36,7 +36,7 @@ constexpr int SCAN_ITEMS = 1024;// rows per block in the row_ptr scan and the bi
 // class it fits: (8,1) (32,1) (32,2) (32,4) (64,4) (64,8).
 constexpr int TINY_NC = 6;
 constexpr int TINY_EBITS = 9;              // numeric sort key = (column << 9) | element (W*K <= 512)
-constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so the numeric tiny classes need N < 2^23 - 1 columns
+constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so a numeric tiny row spans < 2^23 columns (offsets from its first tile)
 __host__ __device__ constexpr int tiny_w(int c) { return c == 0 ? 8 : c <= 3 ? 32 : 64; }
 __host__ __device__ constexpr int tiny_k(int c) { return c <= 1 ? 1 : c == 2 ? 2 : c <= 4 ? 4 : 8; }
 // Symbolic uses the classes below TINY_SYM_NC only (past 128 products a hash table
@@ -280,7 +280,7 @@ struct Work {
     unsigned char* asame;    // M: row has the column pattern of row-1 (k_analyze)
     unsigned char* grp;      // M: row groups (k_bin_list; see RG_MAX)
     int groups;              // form row groups (0: every row alone)
-    int tiny_num;            // numeric tiny classes allowed (B.N <= TINY_NUM_NMAX)
+    int tiny_num;            // numeric tiny classes allowed (per row: column span <= TINY_NUM_NMAX + 1)
     int* bin_list;           // (NUM_NB-1) * M: bin x's rows at (x-1)*M (symbolic bins, then numeric bins)
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count
@@ -300,8 +300,10 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
 void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s);
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
                           Published* pub, int seq);
-void launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
-                    int* Ccol, double* Cval, hipStream_t s, int global_grid, int dense_span_max);
+int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
+                   int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max);
+// numeric launches a call makes for these bin counts (the 32-lane tiny classes share one)
+int numeric_launches(const Stats& h);
 size_t sym_global_bytes_per_block(int N);
 // Device CSR transpose (AAT operand): tmp == nullptr -> *tmp_bytes = scratch size.
 hipError_t transpose_csr(const Csr& A, int* tptr, int* tcol, double* tval, void* tmp, size_t* tmp_bytes,

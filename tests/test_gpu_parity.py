@@ -383,19 +383,31 @@ def test_rocsparse_crosscheck(tool, which):
 
 
 def test_wide_column_space_small_rows(tool):
-    # N > 2^23: the numeric tiny classes are off (packed sort keys hold 23 column bits),
-    # so rows the symbolic phase sorted (tiny) run the table kernels in numeric, with
-    # narrow spans that would qualify for cached tile masks symbolic never wrote
-    rng = np.random.default_rng(12)
-    N = 9_000_000
+    # N > 2^23: the numeric tiny classes pack a column's offset from the row's first tile
+    # into 23 bits, so rows over a narrow span still sort in registers (symbolic sorted them
+    # too: no cached tile masks), at column indices past 2^23
     p, c, v = random_csr(3000, 400, 4, seed=12)
     A = mhspgemm.CSR(3000, 400, p, c, v)
     Bp, Bc, Bv = random_csr(400, 1500, 6, seed=13)
     Bc = (Bc + 8_600_000).astype(np.int32)  # every column past 2^23, within ~24 tiles
-    B = mhspgemm.CSR(400, N, Bp, Bc, Bv)
+    B = mhspgemm.CSR(400, 9_000_000, Bp, Bc, Bv)
     t = check(tool, A, B)
     assert t.sym_bins[5] + t.sym_bins[6] > 0, t.sym_bins
-    assert all(t.num_bins[i] == 0 for i in range(8, 14)), t.num_bins
+    assert sum(t.num_bins[8:12]) > 0, t.num_bins
+
+
+def test_tiny_rows_spanning_past_key_range(tool):
+    # tiny rows whose columns span more than 2^23 (first column near 0, last near 9 M):
+    # their offsets do not fit the packed sort keys, so numeric runs them with tables
+    K, N = 400, 9_000_000
+    rng = np.random.default_rng(5)
+    Bp = np.arange(0, 2 * K + 1, 2, dtype=np.int32)
+    Bc = np.stack([np.arange(K) * 3, 8_900_000 + np.arange(K)], 1).reshape(-1).astype(np.int32)
+    B = mhspgemm.CSR(K, N, Bp, Bc, rng.uniform(0.5, 1.5, 2 * K))
+    p, c, v = random_csr(2000, K, 3, seed=6)
+    A = mhspgemm.CSR(2000, K, p, c, v)
+    t = check(tool, A, B)
+    assert sum(t.num_bins[8:14]) == 0, t.num_bins
 
 
 @pytest.mark.parametrize("per_b", [16, 20])
