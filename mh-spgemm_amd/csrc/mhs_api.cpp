@@ -181,7 +181,7 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list) {
     static_assert((int)NUM_NB >= (int)SYM_NB, "bin_list holds either phase's bins");
     L.bin_list = take((size_t)(NUM_NB - 1) * M * 4);
     L.blkflop = take(((size_t)analyze_blocks(nnzA, M) + 1) * 8);
-    L.scan_part = take(nscan * 8);
+    L.scan_part = take(nscan * 8 + (size_t)CURSOR_INTS * 4);  // look-back words, then the row cursors
     L.mcache = take((size_t)M * mc_stride(mc_list) * 8);
     L.total = o;
     return L;
@@ -368,6 +368,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
     w.nflop = M > 0 ? analyze_blocks(A->nnz, M) : 0;
     w.scan_part = (int*)(ctx->ws + L.scan_part);
+    w.cursors = w.scan_part + 2 * ((M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1);
     w.mcache = ctx->use_mcache ? (unsigned long long*)(ctx->ws + L.mcache) : nullptr;
     w.mc_list = mc_list;
     w.stats = (Stats*)(ctx->ws + L.stats);

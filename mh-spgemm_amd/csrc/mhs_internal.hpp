@@ -28,6 +28,12 @@ constexpr int NBINS = 16;  // capacity of the per-bin counters
 constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
 constexpr int LDS_MAX_C = 163840;  // gfx950: 160 KiB per workgroup (probed on the box)
 constexpr int SCAN_ITEMS = 1024;// rows per block in the row_ptr scan and the bin-list passes
+// Row cursors of the dynamically scheduled bin walks: a launch slot (numeric bin b: b,
+// symbolic bin b: NUM_NB + b) has one cursor per XCD group, 64 bytes apart.  They live after
+// k_scan's look-back words and are zeroed with them by k_analyze.
+constexpr int CURSOR_SLOTS = 40;
+constexpr int CURSOR_STRIDE = 16;  // ints
+constexpr int CURSOR_INTS = CURSOR_SLOTS * 8 * CURSOR_STRIDE;
 
 // Symbolic bins (by LDS need and tile work).
 // Tiny rows: a team of W lanes per row holding K products per lane (flop <= W*K,
@@ -238,8 +244,22 @@ __host__ __device__ inline long long num_need(int span, int t, int n, int dense_
     return m == NM_DENSE ? num_need_dense(span) : m == NM_RMAP ? num_need_rmap(span, n)
                                                : m == NM_DIRECT ? num_need_direct(span, n) : num_need_hash(t, n);
 }
-__host__ __device__ inline bool num_wide(int span, int t, int n, int dense_span_max) {
+#ifndef MHS_SPANRANK
+#define MHS_SPANRANK 1  // hub rows past the 256-thread hash budget: rank tiles by a span bitmap
+#endif
+// Span-bitmap rows (num_row_bitmap): span/64 * 12 bytes + 16 per tile + 8 per C entry.
+__host__ __device__ inline long long num_need_ranked(int span, int t, int n) {
+    const long long nw = ((long long)span + 63) >> 6;
+    return align16(nw * 8) + align16(nw * 4) + 2 * align16((long long)t * 8) + align16((long long)n * 8);
+}
+__host__ __device__ inline bool num_big_hash(int span, int t, int n, int dense_span_max) {
     return num_mode(span, t, n, dense_span_max) == NM_HASH && num_need_hash(t, n) > NUM_B256_BYTES - BLOCK_HDR;
+}
+__host__ __device__ inline bool num_ranked(int span, int t, int n, int dense_span_max) {
+    return MHS_SPANRANK && num_big_hash(span, t, n, dense_span_max) && num_need_ranked(span, t, n) <= B1024_BYTES;
+}
+__host__ __device__ inline bool num_wide(int span, int t, int n, int dense_span_max) {
+    return num_big_hash(span, t, n, dense_span_max) && !num_ranked(span, t, n, dense_span_max);
 }
 // One row's accumulator bytes in mode m (16-aligned); a group of R rows needs the
 // tables once and R accumulators.
@@ -285,6 +305,7 @@ struct Work {
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count
     int* scan_part;    // k_scan's look-back state: one 64-bit word per block (flag | prefix)
+    int* cursors;      // CURSOR_INTS row cursors (after the look-back words)
     unsigned long long* mcache;   // [M][mc_stride] tile masks / tile lists (symbolic -> numeric)
     int mc_list;                  // list cap (see mlisted)
     Stats* stats;

@@ -328,6 +328,38 @@ struct RowWalk {
     }
 };
 
+#ifndef MHS_DYN
+#define MHS_DYN 0  // > 0: wave bins take MHS_DYN consecutive list entries at a time from a cursor
+#endif
+// Dynamic XCD-grouped walk: group g = blockIdx % 8 (an XCD under round-robin dispatch) owns
+// the g-th eighth of the list; its waves take CH consecutive entries at a time from the
+// group's cursor, in list order.  The rows in flight on an XCD stay one compact window
+// (neighbouring rows share B rows in its L2) and a slow row holds back no other.
+struct WaveQueue {
+    int* cur;
+    int begin, end, i, lim, ch;
+    __device__ WaveQueue(int* cursors, int count, int chunk) : ch(chunk) {
+        const int g = (int)(blockIdx.x & 7);
+        begin = (int)((long long)count * g / 8);
+        end = (int)((long long)count * (g + 1) / 8);
+        cur = cursors + g * CURSOR_STRIDE;
+        i = lim = 0;
+    }
+    // next list index of this wave (wave-uniform), false once the group's eighth is done
+    __device__ bool next(int& idx) {
+        if (i >= lim) {
+            int t = 0;
+            if (lane_id() == 0) t = atomicAdd(cur, ch);
+            t = __builtin_amdgcn_readfirstlane(t);
+            i = begin + t;
+            lim = min(i + ch, end);
+            if (i >= end) return false;
+        }
+        idx = i++;
+        return true;
+    }
+};
+
 // ------------------------------------------------------------------- teams ---
 // A team processes one row at a time: a wave (64 lanes, wave_sync) or a whole
 // block (__syncthreads; reductions through an LDS header).  GlobalTeam is a
@@ -1438,6 +1470,59 @@ struct WideTiles {
     }
 };
 
+// ------------------------------------------------------- span bitmap rank ---
+// Rows too big for a 256-thread block's hash table (hub rows of power-law matrices: a
+// few thousand distinct tiles scattered over a span of 10^4..10^5 tiles): a bit per tile
+// of the row's span in LDS and a popcount prefix per 64-bit word give every tile its rank
+// among the row's tiles in O(1) -- no hash, no probe, no CAS, no tile sort -- and per-rank
+// arrays (mask, key, C-row base) hold the row compactly in column order.
+//   walk 1  SpanBits      set the bit of every B tile of the row's products
+//   scan    wpre[w]       = set bits in words < w
+//   walk 2  RankedMasks   OR each B tile's mask into msk[rank], key[rank] = tile
+// LDS: span/64 * 12 bytes + 16 bytes per distinct tile (+ 8 per C entry in numeric).
+__device__ __forceinline__ int span_rank(const unsigned long long* bm, const int* wpre, int d) {
+    return wpre[d >> 6] + (int)__popcll(bm[d >> 6] & ((1ull << (d & 63)) - 1));
+}
+struct SpanBits {
+    static constexpr bool kValues = false;
+    unsigned long long* bm;
+    int lo;
+    const int* __restrict__ btcol;
+    struct Item {
+        int tc;
+        unsigned long long m;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{btcol[i], 0ull}; }
+    __device__ __forceinline__ void put(const Item& x, double) const {
+        const int d = x.tc - lo;
+        atomicOr(&bm[d >> 6], 1ull << (d & 63));
+    }
+};
+struct RankedMasks {
+    static constexpr bool kValues = false;
+    const unsigned long long* bm;
+    const int* wpre;
+    unsigned long long* msk;
+    int2* kb;  // (key, base) per rank
+    int lo;
+    const int* __restrict__ btcol;
+    const unsigned long long* __restrict__ btmask;
+    struct Item {
+        int tc;
+        unsigned long long m;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{btcol[i], btmask[i]}; }
+    __device__ __forceinline__ void put(const Item& x, double) const {
+        const int r = span_rank(bm, wpre, x.tc - lo);
+        atomicOr(&msk[r], x.m);
+        kb[r].x = x.tc;  // every writer of rank r stores the same key
+    }
+};
+__host__ __device__ inline long long span_bits_bytes(int span) {
+    const long long nw = ((long long)span + 63) >> 6;
+    return align16(nw * 8) + align16(nw * 4);
+}
+
 // ------------------------------------------------------------- symbolic ---
 struct SymArgs {
     int M;
@@ -1459,6 +1544,7 @@ struct SymArgs {
     long long gbytes;  // per block
     unsigned long long* mcache;
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
+    int* cursors;            // all row cursors (slot NUM_NB + bin: MHS_DYN)
 };
 
 // Symbolic tile table (counts only, no ranks): masks Mk[H], then -- hashed -- keys Kk[H]:
@@ -1565,6 +1651,11 @@ __device__ __forceinline__ void sym_wave_rows(const SymArgs& a, int bid, int nb)
     const int count = a.stats->sym_count[a.bin];
     const int* list = a.list + (long long)(a.bin - 1) * a.M;
     WaveTeam tm;
+    if (MHS_DYN > 0) {  // (the wave role's blocks are [0, nb) of the launch: bid = blockIdx)
+        WaveQueue q(a.cursors + (NUM_NB + a.bin) * 8 * CURSOR_STRIDE, count, MHS_DYN);
+        for (int li; q.next(li);) sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[li]), E, nullptr);
+        return;
+    }
     for (RowWalk rw(count, WPB, w, bid, nb); rw.first < rw.end; rw.first += rw.stride)
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, nullptr);
 }
@@ -1648,6 +1739,58 @@ __device__ void sym_row_wide(const BlockTeam<1024, false>& tm, const SymArgs& a,
     tm.sync();
 }
 
+// Hashed rare rows whose span bitmap fits: two tile walks (bits, then ranked masks) instead
+// of one walk per window of the span.  Returns false (nothing written) when the span bitmap
+// or the row's tiles do not fit the region; the caller then walks windows.
+__device__ bool sym_row_bitmap(const BlockTeam<1024, false>& tm, const SymArgs& a, int row, char* region,
+                               int4* stage) {
+    constexpr int T = 1024;
+    const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
+    const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
+    const int span = hi - lo + 1;
+    const long long sb = span_bits_bytes(span);
+    if (sb > B1024_BYTES / 2) return false;
+    const int nw = (span + 63) >> 6;
+    unsigned long long* bm = (unsigned long long*)region;
+    int* wpre = (int*)(region + align16((long long)nw * 8));
+    const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
+    const int a0 = __builtin_amdgcn_readfirstlane(a.Aptr[row]), a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
+    for (int i = tm.rank(); i < nw; i += T) bm[i] = 0ull;
+    tm.sync();
+    walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop, SpanBits{bm, lo, a.btcol}, stage);
+    tm.sync();
+    int tl = 0;
+    for (int i = tm.rank(); i < nw; i += T) tl += __popcll(bm[i]);
+    const int t = tm.sum(tl);
+    if (sb + align16((long long)t * 8) * 2 > B1024_BYTES) return false;  // (uniform: every thread returns)
+    tm.exclusive_scan(
+        nw, [&](int i) { return (int)__popcll(bm[i]); }, [&](int i, int v) { wpre[i] = v; });
+    unsigned long long* msk = (unsigned long long*)(region + sb);
+    int2* kb = (int2*)(region + sb + align16((long long)t * 8));
+    for (int r = tm.rank(); r < t; r += T) msk[r] = 0ull;
+    tm.sync();
+    walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop,
+                  RankedMasks{bm, wpre, msk, kb, lo, a.btcol, a.btmask}, stage);
+    tm.sync();
+    long long nl = 0;
+    for (int r = tm.rank(); r < t; r += T) nl += __popcll(msk[r]);
+    const long long n = tm.sum(nl);
+    const int R = __builtin_amdgcn_readfirstlane((int)a.grp[row]);
+    if (tm.rank() < R) {
+        a.Cptr[row + tm.rank()] = (int)n;
+        a.ctiles[row + tm.rank()] = t;
+    }
+    if (a.mcache && mlisted(span, tflop, t, a.mc_list))  // few tiles over a wide span: the list for numeric
+        for (int r = tm.rank(); r < t; r += T)
+            for (int g = 0; g < R; ++g) {
+                unsigned long long* slot = a.mcache + (size_t)(row + g) * a.mc_stride;
+                st_cache(&slot[r], msk[r]);
+                st_cache(&reinterpret_cast<int*>(slot + a.mc_list)[r], kb[r].x);
+            }
+    tm.sync();
+    return true;
+}
+
 __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int4* stage = (int4*)(smem + 1024);
@@ -1662,7 +1805,7 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
             const int span = __builtin_amdgcn_readfirstlane(a.rhi[row]) - __builtin_amdgcn_readfirstlane(a.rlo[row]) + 1;
             if (bin == SYM_B1024 && sym_direct(span, __builtin_amdgcn_readfirstlane(a.rtflop[row])))
                 sym_row(tm, a, row, E, stage);
-            else
+            else if (!(MHS_SPANRANK && sym_row_bitmap(tm, a, row, (char*)E, stage)))
                 sym_row_wide(tm, a, row, (unsigned long long*)E, stage, (int*)(smem + 512));
         }
     }
@@ -1761,7 +1904,8 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
     const bool hash = num_mode(span, t, n, dense_span_max) == NM_HASH;
     if (need <= NUM_WS_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return hash ? NUM_WSH : NUM_WS;
     if (tc >= 0) return NUM_TINY + tc;  // a bigger table than the small wave bin's: sort in registers
-    if (num_wide(span, t, n, dense_span_max)) return NUM_B1024;  // windowed masks, global accumulation
+    if (num_wide(span, t, n, dense_span_max) || num_ranked(span, t, n, dense_span_max))
+        return NUM_B1024;  // rank by span bitmap, else windowed masks with global accumulation
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return hash ? NUM_W16H : NUM_W16;
     if (need <= NUM_B256_BYTES - BLOCK_HDR && flop <= NUM_B256_WORK) return NUM_B256;
     if (need <= B1024_BYTES) return NUM_B1024;
@@ -1959,6 +2103,7 @@ struct NumArgs {
     int dense_span_max;
     const unsigned long long* mcache;
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
+    int* cursor;             // this launch's 8 row cursors (MHS_DYN)
 };
 
 template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
@@ -2317,6 +2462,82 @@ __device__ void num_row_wide(const BlockTeam<T, false>& tm, const NumArgs& a, in
     }
 }
 
+// Numeric rank-by-bitmap row (block kernels): the two tile walks of sym_row_bitmap, the
+// C-row base of every rank by one scan in column order, then each product lands at
+// base[rank] + popc(msk[rank] & below(col)) in an LDS accumulator (no global atomics).
+template <bool GM>
+struct RankAccum {
+    static constexpr bool kValues = true;
+    const unsigned long long* bm;
+    const int* wpre;
+    const unsigned long long* msk;
+    const int2* kb;
+    double* acc;
+    int lo;
+    const int* __restrict__ Bcol;
+    const double* __restrict__ Bval;
+    struct Item {
+        int c;
+        double v;
+    };
+    __device__ __forceinline__ Item load(int i) const { return Item{Bcol[i], Bval[i]}; }
+    __device__ __forceinline__ int col(int i) const { return Bcol[i]; }
+    __device__ __forceinline__ double val(int i) const { return Bval[i]; }
+    __device__ __forceinline__ void put(const Item& x, double a) const { add(x.c, a * x.v); }
+    __device__ __forceinline__ void add(int c, double v) const {
+        const int r = span_rank(bm, wpre, (c >> TILE_SHIFT) - lo);
+        const int idx = kb[r].y + (int)__popcll(msk[r] & ((1ull << (c & (TILE_BITS - 1))) - 1));
+        acc_add<GM>(&acc[idx], v);
+    }
+    template <int RM>
+    __device__ __forceinline__ void add_rows(int, const double (&)[RM], int, int) const {}
+};
+
+template <int T>
+__device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, int row, int lo, int span, int t,
+                               int c0, int n, int a0, int a1, char* region, int4* stage) {
+    const int nw = (span + 63) >> 6;
+    const long long sb = span_bits_bytes(span);
+    unsigned long long* bm = (unsigned long long*)region;
+    int* wpre = (int*)(region + align16((long long)nw * 8));
+    unsigned long long* msk = (unsigned long long*)(region + sb);
+    int2* kb = (int2*)(region + sb + align16((long long)t * 8));
+    double* acc = (double*)(region + sb + 2 * align16((long long)t * 8));
+    const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
+    for (int i = tm.rank(); i < nw; i += T) bm[i] = 0ull;
+    for (int r = tm.rank(); r < t; r += T) msk[r] = 0ull;
+    tm.sync();
+    walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop, SpanBits{bm, lo, a.btcol}, stage);
+    tm.sync();
+    tm.exclusive_scan(
+        nw, [&](int i) { return (int)__popcll(bm[i]); }, [&](int i, int v) { wpre[i] = v; });
+    walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop,
+                  RankedMasks{bm, wpre, msk, kb, lo, a.btcol, a.btmask}, stage);
+    tm.sync();
+    tm.exclusive_scan(
+        t, [&](int r) { return (int)__popcll(msk[r]); }, [&](int r, int v) { kb[r].y = v; });
+    for (int r = tm.rank(); r < n; r += T) acc[r] = 0.0;
+    tm.sync();
+    walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, __builtin_amdgcn_readfirstlane(a.rflop[row]),
+                  RankAccum<false>{bm, wpre, msk, kb, acc, lo, a.Bcol, a.Bval}, stage);
+    tm.sync();
+    for (int r = tm.rank(); r < n; r += T) st_stream(&a.Cval[c0 + r], acc[r]);
+    tm.sync();  // the accumulator region now stages the column indices
+    int* cb = (int*)acc;
+    for (int r = tm.rank(); r < t; r += T) {
+        unsigned long long m = msk[r];
+        const int2 e = kb[r];
+        int b = e.y;
+        while (m) {
+            cb[b++] = (e.x << TILE_SHIFT) + __builtin_ctzll(m);
+            m &= m - 1;
+        }
+    }
+    tm.sync();
+    for (int r = tm.rank(); r < n; r += T) st_stream(&a.Ccol[c0 + r], cb[r]);
+    tm.sync();
+}
+
 // MODES: which row bodies a kernel instantiates (the binning sends a row only to a
 // kernel that has its mode): the hash body's register sort would otherwise set the
 // register budget -- and the occupancy -- of the direct-mapped wave kernels too.
@@ -2357,14 +2578,20 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     const int w = threadIdx.x >> 6;
     char* reg = smem + w * BYTES;
     WaveTeam tm;
-    for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride) {
-        const int row = __builtin_amdgcn_readfirstlane(a.list[rw.first]);
+    auto one = [&](int li) {
+        const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
         if constexpr (GROUPED)  // a group head: R rows of one pattern
             num_row<WaveTeam, false, true, MODES_ALL>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
                                                          __builtin_amdgcn_readfirstlane((int)a.grp[row]));
         else
             num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH>(tm, a, row, reg + WAVE_HDR,
                                                                              (int*)reg, nullptr);
+    };
+    if (MHS_DYN > 0) {
+        WaveQueue q(a.cursor, a.count, MHS_DYN);
+        for (int li; q.next(li);) one(li);
+    } else {
+        for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride) one(rw.first);
     }
 }
 
@@ -2400,6 +2627,11 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
             const int t = __builtin_amdgcn_readfirstlane(a.ctiles[row]);
             const int c0 = __builtin_amdgcn_readfirstlane(a.Cptr[row]);
             const int n = __builtin_amdgcn_readfirstlane(a.Cptr[row + 1]) - c0;
+            if (MHS_SPANRANK && num_ranked(hi - lo + 1, t, n, a.dense_span_max)) {
+                num_row_bitmap<T>(tm, a, row, lo, hi - lo + 1, t, c0, n, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
+                                  __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]), reg, stage);
+                continue;
+            }
             if (num_wide(hi - lo + 1, t, n, a.dense_span_max)) {
                 num_row_wide<T>(tm, a, row, lo, hi, c0, n, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
                                 __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]), reg, stage);
@@ -2688,7 +2920,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS)
+#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2)
     switch (G) {
     case 8: MHS_ANALYZE(8); break;
     case 16: MHS_ANALYZE(16); break;
@@ -2767,6 +2999,7 @@ static SymArgs sym_args(const Csr& A, const Work& w, int M, int N, int* Cptr) {
     a.mcache = w.mcache;
     a.mc_list = w.mc_list;
     a.mc_stride = mc_stride(w.mc_list);
+    a.cursors = w.cursors;
     a.bin = 0;
     return a;
 }
@@ -2860,11 +3093,13 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     a.gscratch = (char*)w.gscratch;
     a.gbytes = 0;
     a.grp = w.grp;
+    a.cursor = w.cursors;
 
     // Largest bins first so the long rows start early.
     if (h.num_count[NUM_GLOBAL] > 0) {
         const int count = a.count = h.num_count[NUM_GLOBAL];
         a.list = w.bin_list + (long long)(NUM_GLOBAL - 1) * A.M;
+        a.cursor = w.cursors + NUM_GLOBAL * 8 * CURSOR_STRIDE;
         a.gbytes = align16(h.num_global_need);
         const int g = count < global_grid ? count : global_grid;
         s = next_stream();
@@ -2873,18 +3108,21 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_B1024] > 0) {
         const int count = a.count = h.num_count[NUM_B1024];
         a.list = w.bin_list + (long long)(NUM_B1024 - 1) * A.M;
+        a.cursor = w.cursors + NUM_B1024 * 8 * CURSOR_STRIDE;
         s = next_stream();
         hipLaunchKernelGGL((k_num_block<1024, false>), dim3(round8(count, 256)), dim3(1024), LDS_MAX - 1024, s, a);
     }
     if (h.num_count[NUM_B256] > 0) {
         const int count = a.count = h.num_count[NUM_B256];
         a.list = w.bin_list + (long long)(NUM_B256 - 1) * A.M;
+        a.cursor = w.cursors + NUM_B256 * 8 * CURSOR_STRIDE;
         s = next_stream();
         hipLaunchKernelGGL((k_num_block<256, false>), dim3(round8(count, 1024)), dim3(256), NUM_B256_BYTES, s, a);
     }
     if (h.num_count[NUM_W16H] > 0) {
         const int count = a.count = h.num_count[NUM_W16H];
         a.list = w.bin_list + (long long)(NUM_W16H - 1) * A.M;
+        a.cursor = w.cursors + NUM_W16H * 8 * CURSOR_STRIDE;
         s = next_stream();
         hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), dim3(round8((count + WPB - 1) / WPB, 2048)),
                            dim3(256), WPB * NUM_W16_BYTES, s, a);
@@ -2892,6 +3130,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_WSH] > 0) {
         const int count = a.count = h.num_count[NUM_WSH];
         a.list = w.bin_list + (long long)(NUM_WSH - 1) * A.M;
+        a.cursor = w.cursors + NUM_WSH * 8 * CURSOR_STRIDE;
         s = next_stream();
         hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
                            dim3(256), WPB * NUM_WS_BYTES, s, a);
@@ -2899,6 +3138,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_W16] > 0) {
         const int count = a.count = h.num_count[NUM_W16];
         a.list = w.bin_list + (long long)(NUM_W16 - 1) * A.M;
+        a.cursor = w.cursors + NUM_W16 * 8 * CURSOR_STRIDE;
         s = next_stream();
         hipLaunchKernelGGL(k_num_wave_direct<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
                            WPB * NUM_W16_BYTES, s, a);
@@ -2945,6 +3185,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_W16G] > 0) {
         const int count = a.count = h.num_count[NUM_W16G];
         a.list = w.bin_list + (long long)(NUM_W16G - 1) * A.M;
+        a.cursor = w.cursors + NUM_W16G * 8 * CURSOR_STRIDE;
         s = next_stream();
         hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true>), dim3(round8((count + WPB - 1) / WPB, 2048)),
                            dim3(256), WPB * NUM_W16_BYTES, s, a);
@@ -2952,6 +3193,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_WSG] > 0) {
         const int count = a.count = h.num_count[NUM_WSG];
         a.list = w.bin_list + (long long)(NUM_WSG - 1) * A.M;
+        a.cursor = w.cursors + NUM_WSG * 8 * CURSOR_STRIDE;
         s = next_stream();
         hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
                            dim3(256), WPB * NUM_WSG_BYTES, s, a);
@@ -2959,6 +3201,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_WS] > 0) {
         const int count = a.count = h.num_count[NUM_WS];
         a.list = w.bin_list + (long long)(NUM_WS - 1) * A.M;
+        a.cursor = w.cursors + NUM_WS * 8 * CURSOR_STRIDE;
         s = next_stream();
         hipLaunchKernelGGL(k_num_wave_direct<NUM_WS_BYTES>, dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
                            dim3(256), WPB * NUM_WS_BYTES, s, a);

@@ -447,3 +447,27 @@ def test_wide_symbolic_rows_few_tiles(tool, spread):
                      rng.uniform(0.1, 1.0, int(Ap[-1])))
     t = check(tool, A, B)
     assert t.sym_bins[3] + t.sym_bins[4] > 0, t.sym_bins
+
+
+@pytest.mark.parametrize("case", ["ranked", "wide"])
+def test_hub_rows_span_rank_and_windows(tool, case):
+    # hub rows (thousands of A entries on short scattered B rows): "ranked" -- a few thousand
+    # distinct tiles over a ~100 k-tile span, past the 256-thread hash budget: symbolic and
+    # numeric rank tiles by a span bitmap in the 1024-thread kernels; "wide" -- ~9 k tiles over
+    # a ~940 k-tile span, whose bitmap does not fit: symbolic walks windows, numeric accumulates
+    # in C with global atomics
+    rng = np.random.default_rng(31)
+    K, N, per = (3000, 6_400_000, 2) if case == "ranked" else (3000, 60_000_000, 3)
+    Bl = np.full(K, per)
+    Bp = np.zeros(K + 1, np.int32)
+    Bp[1:] = np.cumsum(Bl)
+    Bc = np.concatenate([np.sort(rng.choice(N, per, replace=False)) for _ in range(K)]).astype(np.int32)
+    B = mhspgemm.CSR(K, N, Bp, Bc, rng.uniform(0.5, 1.5, int(Bp[-1])))
+    rows = [np.sort(rng.choice(K, 2500 if case == "ranked" else K, replace=False)) for _ in range(6)]
+    rows += [np.sort(rng.choice(K, 4, replace=False)) for _ in range(50)]  # small rows beside them
+    Ap = np.zeros(len(rows) + 1, np.int64)
+    Ap[1:] = np.cumsum([len(r) for r in rows])
+    A = mhspgemm.CSR(len(rows), K, Ap.astype(np.int32), np.concatenate(rows).astype(np.int32),
+                     rng.uniform(0.1, 1.0, int(Ap[-1])))
+    t = check(tool, A, B)
+    assert t.num_bins[4] >= 6, t.num_bins  # the hub rows run in the 1024-thread kernel
