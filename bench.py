@@ -200,31 +200,48 @@ def main():
                 "mem_alloc_ms": round(tc.mem_alloc, 4), "Malloc_C_col_val_ms": round(tc.Malloc_C_col_val, 4)}
     else:
         from mhspgemm import distributed as D
-        rf = D.row_flop(A.ptr, A.col, A.ptr)
-        bnd = D.partition_rows(rf, world)
-        blk = D.local_block(A.ptr, A.col, A.val, int(bnd[rank]), int(bnd[rank + 1]), dev)
-        mult = D.hip_local_multiply(tool)
         from mhspgemm import _lib as L
         tool.set_option(L.MHS_OPT_SYNC, 0)  # stream-ordered calls: no host wait after the numeric launch
-        plan = D.ShardPlan(blk, A.N, mode=args.exchange)  # setup: row plan, buffers (outside the timed steps)
-        for _ in range(args.warmup):
-            C, _ = D.spgemm_planned(plan, mult)
-            C.release()
+        # each rank keeps only its equal-row block of the input (what a rank reading its part
+        # of the file would hold); the flop balance and the exchange plan are built from the
+        # blocks with collectives, timed as plan_ms (setup, outside the steps)
+        r0, r1 = D.equal_rows(A.M, world, rank)
+        eq = D.local_block(A.ptr, A.col, A.val, r0, r1, dev)
+        M_glob = A.M
+        A.release()
         barrier()
-        t0 = time.perf_counter()
-        nloc = 0
-        for _ in range(args.steps):
-            C, _ = D.spgemm_planned(plan, mult)
-            nloc = C.nnz
-            C.release()
+        p0 = time.perf_counter()
+        blk = D.rebalance(eq, M_glob)
+        del eq
+        plan = D.ShardPlan(blk, M_glob, mode=args.exchange)
         barrier()
-        elapsed = time.perf_counter() - t0
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
-        nn = torch.tensor([nloc, plan.bytes_in, plan.nB], dtype=torch.int64, device=dev)
-        dist.all_reduce(nn)
-        nnzC, xbytes, xrows = (int(x) for x in nn.tolist())
+        plan_ms = (time.perf_counter() - p0) * 1e3
+        mult = D.hip_local_multiply(tool)
+
+        def timed(pl):
+            for _ in range(args.warmup):
+                C, _ = D.spgemm_planned(pl, mult)
+                C.release()
+            barrier()
+            t0 = time.perf_counter()
+            nloc = 0
+            for _ in range(args.steps):
+                C, _ = D.spgemm_planned(pl, mult)
+                nloc = C.nnz
+                C.release()
+            barrier()
+            tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            nn = torch.tensor([nloc, pl.bytes_in, pl.nB], dtype=torch.int64, device=dev)
+            dist.all_reduce(nn)
+            return float(tt.item()), [int(x) for x in nn.tolist()]
+
+        t_max, (nnzC, xbytes, xrows) = timed(plan)
+        # the other exchange mode beside it (the north_star's allgatherv when the headline is halo)
+        alt_mode = "full" if args.exchange == "halo" else "halo"
+        alt_plan = D.ShardPlan(blk, M_glob, mode=alt_mode)
+        t_alt, (_, alt_bytes, _) = timed(alt_plan)
+        del alt_plan
         if args.gather:
             tool.set_option(L.MHS_OPT_SYNC, 1)
             C, _ = D.spgemm_planned(plan, mult)
@@ -308,7 +325,12 @@ def main():
         out["roofline"] = None
         out["cpu_baseline"] = None
         out["exchange"] = {"mode": args.exchange, "bytes_in_per_step_all_ranks": xbytes,
-                           "local_B_rows_all_ranks": xrows}
+                           "local_B_rows_all_ranks": xrows, "plan_ms": round(plan_ms, 3),
+                           "plan": "distributed flop balance from equal-row blocks (mhspgemm.distributed.rebalance) "
+                                   "+ ShardPlan, collectives only, timed once before the steps"}
+        ms_alt = t_alt / args.steps * 1e3
+        out["exchange_alt"] = {"mode": alt_mode, "value": round(2.0 * flop / (ms_alt * 1e-3) / 1e9, 2),
+                               "ms_per_step": round(ms_alt, 4), "bytes_in_per_step_all_ranks": alt_bytes}
         if gather_ms is not None:
             out["gather_C_ms"] = round(gather_ms, 3)
     print(json.dumps(out), flush=True)

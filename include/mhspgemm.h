@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 4
+#define MHS_ABI_VERSION 5
 
 typedef enum mhs_status {
     MHS_OK = 0,
@@ -92,12 +92,29 @@ int mhs_ctx_trim(mhs_ctx *ctx);
  *     nnz and arrays are valid; their contents are stream-ordered, as for any
  *     kernel output).  A call with a timing struct always synchronises.
  *   MHS_OPT_NUMERIC_EVENTS (default 0): keep hipEvent pairs around the numeric
- *     phase of the last `value` calls, read with mhs_ctx_numeric_ms. */
-typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2 } mhs_option;
+ *     phase of the last `value` calls, read with mhs_ctx_numeric_ms.
+ *   MHS_OPT_MEM_BUDGET (default 0 = none): treat a call's workspace, or workspace
+ *     plus C, beyond `value` MiB as an out-of-memory condition (exercises the
+ *     row-chunked fallback below without filling the device).
+ * Out of memory: when the workspace, or C beside it, does not fit, mhs_spgemm gives
+ * back every cached buffer and retries row-chunked (the workspace sized for half the
+ * rows, halved until it fits; C sized by a counting pass and allocated once); it
+ * returns MHS_ERR_OOM only when C itself or a one-row workspace does not fit. */
+typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2, MHS_OPT_MEM_BUDGET = 3 } mhs_option;
 int mhs_ctx_set_option(mhs_ctx *ctx, int option, int value);
+/* Calls of this context that ran row-chunked (the out-of-memory fallback). */
+long long mhs_ctx_chunked_calls(const mhs_ctx *ctx);
 /* Numeric-phase durations (ms) of the last min(n, recorded) calls, oldest
  * first; waits for them.  Returns the count written, or -status on error. */
 int mhs_ctx_numeric_ms(mhs_ctx *ctx, float *out, int n);
+
+/* Hash probe conflicts (the reference's HASH_CONFLICT switch, inc/common.h:18, printed
+ * at src/main.cu:68-71): probe steps that met another key in the symbolic and numeric
+ * tile hash tables (inserts and lookups) since the previous call of this function, which
+ * resets the count.  Only the diagnostic library libmhspgemm_probe.so (built with
+ * MHS_PROBE_STATS=1) counts; the product library returns MHS_ERR_INVALID.  Synchronises
+ * the context stream.  The counter is per process (shared by all contexts). */
+int mhs_probe_conflicts(mhs_ctx *ctx, uint64_t *count);
 
 /* C = A * B on the device.  A, B: device CSR.  On MHS_OK, C->M = A->M,
  * C->N = B->N, C->nnz is set and C->ptr/col/val are fresh device

@@ -48,6 +48,8 @@ struct mhs_ctx {
     bool stats_zero = false; // the workspace's device Stats are zero (left so by the last k_scan)
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     bool tiny_num = true;    // numeric tiny (sort) classes (MHS_NO_TINY_NUM=1: off)
+    size_t mem_budget = 0;   // MHS_OPT_MEM_BUDGET (MiB): a call's workspace + C beyond it count as OOM (tests)
+    long long chunked_calls = 0;  // calls that ran row-chunked (mhs_ctx_chunked_calls)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays): (buffer, allocation size)
     std::vector<std::pair<void*, size_t>> pool;
@@ -195,13 +197,234 @@ int ensure(mhs_ctx* ctx, char** buf, size_t* have, size_t need) {
         *buf = nullptr;
         *have = 0;
     }
-    const size_t want = need + need / 8;
+    size_t want = need + need / 8;
+    if (ctx->mem_budget && want > ctx->mem_budget) want = need;
+    if (ctx->mem_budget && need > ctx->mem_budget)
+        return fail(ctx, MHS_ERR_OOM, "workspace exceeds the context's memory budget");
     MHS_HIP(hipMalloc((void**)buf, want));
     *have = want;
     return MHS_OK;
 }
 
+// C.col / C.val of nnz entries (+ what the call already holds) within the test budget
+hipError_t alloc_c(mhs_ctx* ctx, mhs_csr* out, long long nnz) {
+    if (ctx->mem_budget && ctx->ws_bytes + (size_t)nnz * 12 > ctx->mem_budget) return hipErrorOutOfMemory;
+    hipError_t e = pool_get(ctx, (void**)&out->col, (size_t)nnz * 4);
+    if (e == hipSuccess) e = pool_get(ctx, (void**)&out->val, (size_t)nnz * 8);
+    if (e != hipSuccess) {
+        pool_put(ctx, out->col);
+        out->col = nullptr;
+    }
+    return e;
+}
+
+// The call's Work over the workspace laid out by `L` (rows of this pass: M).
+Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, int Bn, int mc_list) {
+    Work w{};
+    w.btcol = (int*)(ctx->ws + L.btcol);
+    w.btmask = (unsigned long long*)(ctx->ws + L.btmask);
+    w.bmeta = (int4*)(ctx->ws + L.bmeta);
+    w.bhi = (int*)(ctx->ws + L.bhi);
+    w.rflop = (int*)(ctx->ws + L.rflop);
+    w.rtflop = (int*)(ctx->ws + L.rtflop);
+    w.rlo = (int*)(ctx->ws + L.rlo);
+    w.rhi = (int*)(ctx->ws + L.rhi);
+    w.ctiles = (int*)(ctx->ws + L.ctiles);
+    w.sym_bin = (unsigned char*)(ctx->ws + L.sym_bin);
+    w.asame = (unsigned char*)(ctx->ws + L.asame);
+    w.grp = (unsigned char*)(ctx->ws + L.grp);
+    w.groups = ctx->groups ? 1 : 0;
+    w.tiny_num = ctx->tiny_num ? 1 : 0;  // per row: packed sort keys hold its column offsets in 23 bits
+    (void)Bn;
+    w.bin_list = (int*)(ctx->ws + L.bin_list);
+    w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
+    w.nflop = M > 0 ? analyze_blocks(nnzA, M) : 0;
+    w.scan_part = (int*)(ctx->ws + L.scan_part);
+    w.cursors = w.scan_part + 2 * ((M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1);
+    w.mcache = ctx->use_mcache ? (unsigned long long*)(ctx->ws + L.mcache) : nullptr;
+    w.mc_list = mc_list;
+    w.stats = (Stats*)(ctx->ws + L.stats);
+    w.gscratch = ctx->gscratch;
+    w.gscratch_bytes = ctx->gscratch_bytes;
+    return w;
+}
+
+std::string err_text(int err) {
+    std::string m;
+    if (err & ERR_UNSORTED) m += "B column indices are not sorted within a row; ";
+    if (err & ERR_COL_RANGE) m += "B column index out of [0, B.N); ";
+    if (err & ERR_ACOL_RANGE) m += "A column index out of [0, B.M); ";
+    if (err & ERR_OVERFLOW) m += "nnz(C) exceeds INT32_MAX; ";
+    return m;
+}
+
+// Everything before the numeric launches for the rows of `a` (M > 0): (mask of B), row
+// analysis, symbolic bins, row_ptr scan into Cptr[0..M] + numeric bins, the Stats hand-off.
+int front_pass(mhs_ctx* ctx, const Csr& a, const Csr& b, Work& w, int* Cptr, bool mask, Stats& h) {
+    hipStream_t s = ctx->stream;
+    if (!ctx->stats_zero) MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
+    ctx->stats_zero = false;
+    if (mask) launch_mask_b(b, w, s);
+    launch_analyze(a, w, b.M, s, Cptr);
+    launch_symbolic_common(a, b, w, a.M, b.N, Cptr, s);
+    launch_symbolic_rare(a, w, a.M, b.N, Cptr, s);
+    const int seq = ++ctx->seq;
+    launch_scan_classify(a.M, w, Cptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
+    MHS_HIP(hipGetLastError());
+    const int rc = wait_published(ctx, s, ctx->pub, seq);
+    if (rc) return rc;
+    memcpy(&h, (const void*)&ctx->pub->stats, sizeof(Stats));
+    ctx->stats_zero = true;
+    return MHS_OK;
+}
+
+// Global-bin scratch for the numeric pass of `h` (grown on demand).
+int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h);
+
 constexpr int NUM_GLOBAL_GRID = 128;
+
+int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h) {
+    if (h.num_count[NUM_GLOBAL] <= 0) return MHS_OK;
+    const size_t per = (size_t)align16(h.num_global_need);
+    const size_t g = (size_t)std::min(h.num_count[NUM_GLOBAL], NUM_GLOBAL_GRID);
+    const int rc = ensure(ctx, &ctx->gscratch, &ctx->gscratch_bytes, per * g);
+    if (rc) return rc;
+    w.gscratch = ctx->gscratch;
+    w.gscratch_bytes = ctx->gscratch_bytes;
+    return MHS_OK;
+}
+
+void free_cached(mhs_ctx* ctx) {
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->gscratch) (void)hipFree(ctx->gscratch);
+    ctx->ws = ctx->gscratch = nullptr;
+    ctx->ws_bytes = ctx->gscratch_bytes = 0;
+    for (auto& b : ctx->pool) (void)hipFree(b.first);
+    ctx->pool.clear();
+    ctx->stats_zero = false;
+}
+
+// Row-chunked product, the fallback when the workspace (or the workspace and C together)
+// does not fit the device: everything cached is given back, the workspace is laid out for
+// Mc rows (halved until it fits), a counting pass over the chunks sizes C, C is allocated
+// once, and a second pass writes every chunk's rows at their offset in C (row_ptr rebased
+// by one small kernel per chunk).  The reference has no such path: Tool::allocate and the
+// C cudaMalloc simply throw (src/Tool.cu:4-45, src/main.cu:54-61).
+int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs_timing* t,
+                   std::chrono::steady_clock::time_point T0) {
+    const int M = A->M, MB = B->M;
+    hipStream_t s = ctx->stream;
+    MHS_HIP(hipStreamSynchronize(s));
+    free_cached(ctx);
+    (void)hipGetLastError();
+    int Mc = M, mc_list = 0;
+    Layout L{};
+    const Csr b{B->M, B->N, B->nnz, B->ptr, B->col, B->val};
+    auto view = [&](int c) {
+        const int r0 = c * Mc, r1 = std::min(M, r0 + Mc);
+        // nnz of a view only steers launch geometry: the same estimate in plan and launch
+        const int est = (int)((long long)A->nnz * (r1 - r0) / (M > 0 ? M : 1));
+        return Csr{r1 - r0, A->N, est, A->ptr + r0, A->col, A->val};
+    };
+    int nch = 0;
+    Stats h{};
+    long long total = 0;
+    unsigned long long flop = 0;
+    mhs_csr out{};
+    for (;;) {  // halve the chunk until the workspace and then C fit
+        if (Mc <= 1) return fail(ctx, MHS_ERR_OOM, "C and a one-row workspace do not fit the device");
+        Mc = (Mc + 1) / 2;
+        if (ctx->ws) (void)hipFree(ctx->ws);
+        ctx->ws = nullptr;
+        ctx->ws_bytes = 0;
+        ctx->stats_zero = false;
+        mc_list = ctx->mc_list > 0 ? ctx->mc_list : mc_list_for(Mc);
+        L = plan(Mc, MB, A->nnz, B->nnz, mc_list);
+        int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
+        if (rc == MHS_ERR_OOM) {
+            (void)hipGetLastError();
+            continue;
+        }
+        if (rc) return rc;
+        // pass 1: counts
+        nch = (M + Mc - 1) / Mc;
+        int* tptr = nullptr;
+        MHS_HIP(pool_get(ctx, (void**)&tptr, (size_t)(Mc + 1) * 4));
+        total = 0;
+        flop = 0;
+        for (int c = 0; c < nch; ++c) {
+            const Csr a = view(c);
+            Work w = make_work(ctx, L, a.M, a.nnz, B->N, mc_list);
+            rc = front_pass(ctx, a, b, w, tptr, c == 0, h);
+            if (rc == MHS_OK && h.err)
+                rc = fail(ctx, (h.err & ERR_OVERFLOW) ? MHS_ERR_OVERFLOW : MHS_ERR_INVALID, err_text(h.err));
+            if (rc) {
+                pool_put(ctx, tptr);
+                return rc;
+            }
+            total += h.nnzC;
+            flop += h.flop;
+        }
+        pool_put(ctx, tptr);
+        if (total > INT_MAX) return fail(ctx, MHS_ERR_OVERFLOW, "nnz(C) exceeds INT32_MAX");
+        out = mhs_csr{};
+        out.M = M;
+        out.N = B->N;
+        out.nnz = (int)total;
+        hipError_t e = pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4);
+        if (e == hipSuccess) e = alloc_c(ctx, &out, total);
+        if (e == hipSuccess) break;
+        pool_put(ctx, out.ptr);
+        (void)hipGetLastError();
+        if (e != hipErrorOutOfMemory) return fail_hip(ctx, e, "allocating C (row-chunked)");
+        for (auto& bf : ctx->pool) (void)hipFree(bf.first);
+        ctx->pool.clear();
+    }
+    // pass 2: every chunk's rows at their offset
+    long long off = 0;
+    int sym[NBINS] = {}, num[NBINS] = {};
+    for (int c = 0; c < nch; ++c) {
+        const Csr a = view(c);
+        const int r0 = c * Mc;
+        Work w = make_work(ctx, L, a.M, a.nnz, B->N, mc_list);
+        int rc = front_pass(ctx, a, b, w, out.ptr + r0, false, h);
+        if (rc == MHS_OK) rc = ensure_gscratch(ctx, w, h);
+        if (rc) {
+            mhs_ctx_recycle(ctx, &out);
+            return rc;
+        }
+        if (h.nnzC > 0)
+            launch_numeric(a, b, w, h, out.ptr + r0, out.col + off, out.val + off, &s, 1, NUM_GLOBAL_GRID,
+                           ctx->dense_span_max);
+        launch_add_offset(out.ptr + r0, a.M + (c == nch - 1 ? 1 : 0), (int)off, s);
+        MHS_HIP(hipGetLastError());
+        off += h.nnzC;
+        for (int i = 1; i < NBINS; ++i) {
+            sym[i] += h.sym_count[i];
+            num[i] += h.num_count[i];
+        }
+    }
+    MHS_HIP(hipStreamSynchronize(s));
+    *C = out;
+    ++ctx->chunked_calls;
+    if (t) {
+        mhs_timing tm{};
+        tm.total_e2e = tm.total_ref = ms_since(T0);
+        tm.flop = flop;
+        tm.nnzC = total;
+        long long ns = 0, nn = 0;
+        for (int i = 1; i < 16; ++i) {
+            tm.sym_bins[i] = i < NBINS ? sym[i] : 0;
+            tm.num_bins[i] = i < NBINS ? num[i] : 0;
+            ns += tm.sym_bins[i];
+            nn += tm.num_bins[i];
+        }
+        tm.sym_bins[0] = (int)(M - ns);
+        tm.num_bins[0] = (int)(M - nn);
+        *t = tm;
+    }
+    return MHS_OK;
+}
 
 
 }  // namespace
@@ -346,34 +569,11 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     const Layout L = plan(M, MB, A->nnz, B->nnz, mc_list);
     const char* ws_before = ctx->ws;
     int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
+    if (rc == MHS_ERR_OOM && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
     if (rc) return rc;
     if (ctx->ws != ws_before) ctx->stats_zero = false;
     MHS_HIP(pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4));
-    Work w{};
-    w.btcol = (int*)(ctx->ws + L.btcol);
-    w.btmask = (unsigned long long*)(ctx->ws + L.btmask);
-    w.bmeta = (int4*)(ctx->ws + L.bmeta);
-    w.bhi = (int*)(ctx->ws + L.bhi);
-    w.rflop = (int*)(ctx->ws + L.rflop);
-    w.rtflop = (int*)(ctx->ws + L.rtflop);
-    w.rlo = (int*)(ctx->ws + L.rlo);
-    w.rhi = (int*)(ctx->ws + L.rhi);
-    w.ctiles = (int*)(ctx->ws + L.ctiles);
-    w.sym_bin = (unsigned char*)(ctx->ws + L.sym_bin);
-    w.asame = (unsigned char*)(ctx->ws + L.asame);
-    w.grp = (unsigned char*)(ctx->ws + L.grp);
-    w.groups = ctx->groups ? 1 : 0;
-    w.tiny_num = ctx->tiny_num ? 1 : 0;  // per row: packed sort keys hold its column offsets in 23 bits
-    w.bin_list = (int*)(ctx->ws + L.bin_list);
-    w.blkflop = (unsigned long long*)(ctx->ws + L.blkflop);
-    w.nflop = M > 0 ? analyze_blocks(A->nnz, M) : 0;
-    w.scan_part = (int*)(ctx->ws + L.scan_part);
-    w.cursors = w.scan_part + 2 * ((M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1);
-    w.mcache = ctx->use_mcache ? (unsigned long long*)(ctx->ws + L.mcache) : nullptr;
-    w.mc_list = mc_list;
-    w.stats = (Stats*)(ctx->ws + L.stats);
-    w.gscratch = ctx->gscratch;
-    w.gscratch_bytes = ctx->gscratch_bytes;
+    Work w = make_work(ctx, L, M, A->nnz, B->N, mc_list);
     // device Stats start zeroed: the previous call's k_scan left them so, else a memset
     if (!ctx->stats_zero) MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
     ctx->stats_zero = false;  // until this call's k_scan has published and cleared them
@@ -435,24 +635,19 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // ---- Malloc_C_col_val ---------------------------------------------------------------
     const auto T5 = std::chrono::steady_clock::now();
     {
-        hipError_t e = pool_get(ctx, (void**)&out.col, (size_t)out.nnz * 4);
-        if (e == hipSuccess) e = pool_get(ctx, (void**)&out.val, (size_t)out.nnz * 8);
+        const hipError_t e = alloc_c(ctx, &out, out.nnz);
         if (e != hipSuccess) {
             pool_put(ctx, out.ptr);
-            pool_put(ctx, out.col);
+            (void)hipGetLastError();
+            // C beside the full workspace does not fit: retry with a row-chunked workspace
+            if (e == hipErrorOutOfMemory && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
             return fail_hip(ctx, e, "allocating C.col/C.val");
         }
     }
-    if (h.num_count[NUM_GLOBAL] > 0) {
-        const size_t per = (size_t)align16(h.num_global_need);
-        const size_t g = (size_t)std::min(h.num_count[NUM_GLOBAL], NUM_GLOBAL_GRID);
-        rc = ensure(ctx, &ctx->gscratch, &ctx->gscratch_bytes, per * g);
-        if (rc) {
-            mhs_ctx_recycle(ctx, &out);
-            return rc;
-        }
-        w.gscratch = ctx->gscratch;
-        w.gscratch_bytes = ctx->gscratch_bytes;
+    rc = ensure_gscratch(ctx, w, h);
+    if (rc) {
+        mhs_ctx_recycle(ctx, &out);
+        return rc;
     }
     const double t_malloc = ms_since(T5);
 
@@ -566,10 +761,16 @@ int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
         ctx->ncalls = 0;
         return MHS_OK;
     }
+    case MHS_OPT_MEM_BUDGET:
+        if (value < 0) return fail(ctx, MHS_ERR_INVALID, "memory budget must be >= 0 MiB");
+        ctx->mem_budget = (size_t)value << 20;
+        return MHS_OK;
     default:
         return fail(ctx, MHS_ERR_INVALID, "unknown option");
     }
 }
+
+long long mhs_ctx_chunked_calls(const mhs_ctx* ctx) { return ctx ? ctx->chunked_calls : -1; }
 
 int mhs_ctx_numeric_ms(mhs_ctx* ctx, float* out, int n) {
     if (!ctx || (!out && n > 0)) return -MHS_ERR_INVALID;
@@ -586,6 +787,20 @@ int mhs_ctx_numeric_ms(mhs_ctx* ctx, float* out, int n) {
         out[i] = f;
     }
     return (int)have;
+}
+
+int mhs_probe_conflicts(mhs_ctx* ctx, uint64_t* count) {
+    if (!ctx || !count) return MHS_ERR_INVALID;
+    unsigned long long* dev = nullptr;
+    MHS_HIP(hipSetDevice(ctx->device));
+    MHS_HIP(probe_counter(&dev));
+    if (!dev) return fail(ctx, MHS_ERR_INVALID, "probe statistics need the MHS_PROBE_STATS=1 build (libmhspgemm_probe.so)");
+    unsigned long long v = 0;
+    MHS_HIP(hipMemcpyAsync(&v, dev, sizeof v, hipMemcpyDeviceToHost, ctx->stream));
+    MHS_HIP(hipMemsetAsync(dev, 0, sizeof v, ctx->stream));
+    MHS_HIP(hipStreamSynchronize(ctx->stream));
+    *count = v;
+    return MHS_OK;
 }
 
 int mhs_memcpy(mhs_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {

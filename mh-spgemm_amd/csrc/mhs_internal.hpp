@@ -326,9 +326,13 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
 // numeric launches a call makes for these bin counts (the 32-lane tiny classes share one)
 int numeric_launches(const Stats& h);
 size_t sym_global_bytes_per_block(int N);
+// p[0..n) += off (row-chunked products: a chunk's row_ptr rebased to its place in C)
+void launch_add_offset(int* p, int n, int off, hipStream_t s);
 // Device CSR transpose (AAT operand): tmp == nullptr -> *tmp_bytes = scratch size.
 hipError_t transpose_csr(const Csr& A, int* tptr, int* tcol, double* tval, void* tmp, size_t* tmp_bytes,
                          hipStream_t s);
 hipError_t init_kernel_attributes();
+// device address of the probe-conflict counter (nullptr unless built with MHS_PROBE_STATS=1)
+hipError_t probe_counter(unsigned long long** dev);
 
 }  // namespace mhs

@@ -54,6 +54,9 @@
 #ifndef MHS_VAL_GMIN
 #define MHS_VAL_GMIN 4  // narrowest lane group of a value walk
 #endif
+#ifndef MHS_TILE_GMIN
+#define MHS_TILE_GMIN 4  // narrowest lane group of a tile walk
+#endif
 #ifndef MHS_RUN_GMIN
 #define MHS_RUN_GMIN 32  // narrowest lane group of a chunk with merged runs
 #endif
@@ -170,6 +173,22 @@ __device__ __forceinline__ long long wave_incl_scan64(long long x) {
 __device__ __forceinline__ unsigned long long lanemask_lt() {
     const int lane = lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// Opt-in probe statistics (the reference's HASH_CONFLICT, inc/common.h:18, printed at
+// src/main.cu:68-71): a build with MHS_PROBE_STATS=1 counts every probe step that met
+// another key -- symbolic inserts, numeric table builds and numeric lookups -- in one
+// device counter read back by mhs_probe_count().  Off (and free) in the product build.
+#ifndef MHS_PROBE_STATS
+#define MHS_PROBE_STATS 0
+#endif
+#if MHS_PROBE_STATS
+__device__ unsigned long long g_probe_conflicts;
+#endif
+__device__ __forceinline__ void probe_conflict() {
+#if MHS_PROBE_STATS
+    atomicAdd(&g_probe_conflicts, 1ull);
+#endif
 }
 
 // Fibonacci hash of a tile key into [0, H) (any H: multiply-high range reduction)
@@ -328,6 +347,10 @@ struct RowWalk {
     }
 };
 
+#ifndef MHS_WAVE_CHUNKS
+#define MHS_WAVE_CHUNKS 0  // > 0: block teams walk rows of >= this many A entries per thread wave-by-wave
+                           // (measured: webbase-like numeric +10%, wb-edu-like symbolic -8%: off)
+#endif
 #ifndef MHS_DYN
 #define MHS_DYN 0  // > 0: wave bins take MHS_DYN consecutive list entries at a time from a cursor
 #endif
@@ -946,14 +969,13 @@ __device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int 
     }
 }
 
+// One wave's chunks of an A row: [jb0, jb0 + 64), [jb0 + jstep, ...), ... below a1.
 template <class F>
-__device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
-                                             const int* __restrict__ Acol,
-                                             const double* __restrict__ Aval,
-                                             const int4* __restrict__ bmeta, bool tiles, int Grow,
-                                             const F& f, int4*) {
+__device__ __forceinline__ void wave_chunks(int jb0, int jstep, int a1, const int* __restrict__ Acol,
+                                            const double* __restrict__ Aval, const int4* __restrict__ bmeta,
+                                            bool tiles, int Grow, const F& f) {
     const int lane = lane_id();
-    for (int jb = a0; jb < a1; jb += 64) {
+    for (int jb = jb0; jb < a1; jb += jstep) {
         const StagedChunk x = stage_chunk(lane, jb, a1, Acol, Aval, bmeta, tiles);
         // a chunk with merged runs loads LM rows per lane and sweep: wider groups
         // keep each load instruction within fewer cache lines
@@ -992,6 +1014,16 @@ __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
             }
         }
     }
+}
+
+
+template <class F>
+__device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
+                                             const int* __restrict__ Acol,
+                                             const double* __restrict__ Aval,
+                                             const int4* __restrict__ bmeta, bool tiles, int Grow,
+                                             const F& f, int4*) {
+    wave_chunks(a0, 64, a1, Acol, Aval, bmeta, tiles, Grow, f);
 }
 
 // Row group (wave teams only): the head row's A entries are staged as usual and lane
@@ -1298,9 +1330,16 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
     const int nA = a1 - a0;
     if (MHS_NUM_DIAG == 6 && nA > 0 && work >= 8LL * nA)  // flattened walk: experiment only (slower)
         for_products_flat(tm, a0, a1, Acol, Aval, bmeta, tiles, f, stage);
+    else if (Team::size > 64 && MHS_WAVE_CHUNKS > 0 && nA >= MHS_WAVE_CHUNKS * Team::size)
+        // long A rows (hubs of power-law matrices: thousands of entries on short B rows): every
+        // wave walks its own 64-entry chunks wv, wv + W, ... of the row -- no stage, no barrier
+        // (a staged round chains A entry -> bmeta -> B load round trips behind two barriers
+        // per 64*STAGE_SUBS entries)
+        wave_chunks(a0 + 64 * (tm.rank() >> 6), Team::size, a1, Acol, Aval, bmeta, tiles,
+                    pick_group(work, nA, 64, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN), f);
     else
         for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
-                     pick_group(work, nA, Team::size, tiles ? 4 : MHS_VAL_GMIN), f, stage);
+                     pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN), f, stage);
 }
 
 // ---------------------------------------------------------- tile tables ---
@@ -1331,6 +1370,7 @@ struct TileBuild {
                     atomicOr(&E[s].mask, x.m);
                     break;
                 }
+                probe_conflict();
                 s = hnext(s, H);
             }
         }
@@ -1415,6 +1455,7 @@ struct Accum {
             uint4 q = *reinterpret_cast<const uint4*>(&E[s]);  // one ds_read_b128: mask, base, key
             if constexpr (MODE == NM_HASH) {
                 while ((int)q.w != tc) {
+                    probe_conflict();
                     s = hnext(s, H);
                     q = *reinterpret_cast<const uint4*>(&E[s]);
                 }
@@ -1573,6 +1614,7 @@ struct SymTileBuild {
                     atomicOr(&Mk[s], x.m);
                     break;
                 }
+                probe_conflict();
                 s = hnext(s, H);
             }
         }
@@ -2160,7 +2202,10 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                 E[key - lo].mask = m;
             } else {
                 int sl = hslot(key, H);
-                while (atomicCAS(&E[sl].key, -1, key) != -1) sl = hnext(sl, H);  // keys are distinct
+                while (atomicCAS(&E[sl].key, -1, key) != -1) {  // keys are distinct
+                    probe_conflict();
+                    sl = hnext(sl, H);
+                }
                 E[sl].mask = m;
                 if (rank_count) reinterpret_cast<int2*>(acc)[r] = make_int2(key, (sl << 8) | __popcll(m));
             }
@@ -2240,7 +2285,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
         tm.sync();
         for (int i = tm.rank(); i < t; i += Team::size) {
             const int2 me = L[i];
-            int base = 0, j = 0;
+            int base = 0, j = MHS_NUM_DIAG == 10 ? t : 0;  // diag 10: ranking skipped (timing only)
             for (; j + 1 < t; j += 2) {  // two entries per broadcast read
                 const int4 o = *reinterpret_cast<const int4*>(&L[j]);
                 base += (o.x < me.x ? (o.y & 0xFF) : 0) + (o.z < me.x ? (o.w & 0xFF) : 0);
@@ -2932,6 +2977,15 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
                        w.asame, w.grp, w.groups, w.stats->sym_count, w.bin_list);
 }
 
+hipError_t probe_counter(unsigned long long** dev) {
+#if MHS_PROBE_STATS
+    return hipGetSymbolAddress((void**)dev, HIP_SYMBOL(g_probe_conflicts));
+#else
+    *dev = nullptr;
+    return hipSuccess;
+#endif
+}
+
 hipError_t init_kernel_attributes() {
     // gfx950 grants up to 160 KiB of LDS per workgroup; make the large dynamic
     // requests explicit for the block-per-row kernels (which use no static LDS).
@@ -2955,6 +3009,14 @@ hipError_t init_kernel_attributes() {
         e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     return e;
+}
+
+__global__ __launch_bounds__(256) void k_add_offset(int* __restrict__ p, int n, int off) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] += off;
+}
+void launch_add_offset(int* p, int n, int off, hipStream_t s) {
+    if (n <= 0 || off == 0) return;
+    hipLaunchKernelGGL(k_add_offset, dim3(std::min((n + 255) / 256, 4096)), dim3(256), 0, s, p, n, off);
 }
 
 size_t sym_global_bytes_per_block(int N) {

@@ -24,6 +24,7 @@ MHS_ERR_IO = 5
 
 MHS_OPT_SYNC = 1
 MHS_OPT_NUMERIC_EVENTS = 2
+MHS_OPT_MEM_BUDGET = 3
 
 STATUS_NAMES = {0: "MHS_OK", 1: "MHS_ERR_HIP", 2: "MHS_ERR_OOM", 3: "MHS_ERR_INVALID",
                 4: "MHS_ERR_OVERFLOW", 5: "MHS_ERR_IO"}
@@ -114,6 +115,10 @@ def lib() -> ctypes.CDLL:
     L.mhs_device_free.restype = c_int
     L.mhs_transpose.argtypes = [c_void_p, P(mhs_csr), P(mhs_csr)]
     L.mhs_transpose.restype = c_int
+    L.mhs_probe_conflicts.argtypes = [c_void_p, P(ctypes.c_uint64)]
+    L.mhs_probe_conflicts.restype = c_int
+    L.mhs_ctx_chunked_calls.argtypes = [c_void_p]
+    L.mhs_ctx_chunked_calls.restype = ctypes.c_longlong
     _lib = L
     return L
 

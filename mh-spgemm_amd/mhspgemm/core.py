@@ -70,6 +70,17 @@ class Tool:
             _check(self.ctx, -k, "mhs_ctx_numeric_ms")
         return [float(buf[i]) for i in range(k)]
 
+    def probe_conflicts(self) -> int:
+        """Hash probe conflicts since the last query (the reference's HASH_CONFLICT count,
+        src/main.cu:68-71); needs the diagnostic library (MHS_LIB=.../libmhspgemm_probe.so)."""
+        v = ctypes.c_uint64()
+        _check(self.ctx, L.lib().mhs_probe_conflicts(self.ctx, ctypes.byref(v)), "mhs_probe_conflicts")
+        return int(v.value)
+
+    def chunked_calls(self) -> int:
+        """Calls that ran row-chunked (the out-of-memory fallback)."""
+        return int(L.lib().mhs_ctx_chunked_calls(self.ctx))
+
     def allocate(self, B=None, C=None):  # src/Tool.cu:4 -- workspace grows on demand
         return None
 

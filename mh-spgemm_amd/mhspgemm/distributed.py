@@ -5,7 +5,10 @@ ROCm; "gloo" for CPU tests).  The reference is single-GPU; this is the
 north_star's multi-GPU mode:
 
   1. partition   contiguous A row ranges balanced by flop (products), cut at
-                 p*F/P of the int64 prefix sum of per-row flop;
+                 p*F/P of the int64 prefix sum of per-row flop -- `rebalance`
+                 computes the cuts from the ranks' own (equal-row) blocks plus
+                 the all-gathered row lengths and moves rows to their owners,
+                 so no rank needs the whole matrix;
   2. exchange    every rank holds its row block of B (B = A for A*A) and needs
                  the B rows its A block references.  Two executors of one plan:
                  * "halo" (default): a rank receives only the rows its columns
@@ -76,6 +79,104 @@ def local_block(ptr: np.ndarray, col: np.ndarray, val: np.ndarray, r0: int, r1: 
     p = torch.from_numpy((ptr[r0:r1 + 1].astype(np.int64) - s).astype(np.int32)).to(device)
     return Block(r0, r1, p, torch.from_numpy(np.ascontiguousarray(col[s:e])).to(device),
                  torch.from_numpy(np.ascontiguousarray(val[s:e])).to(device))
+
+
+def equal_rows(M: int, P: int, p: int):
+    """Rows [M*p/P, M*(p+1)/P): the block a rank loads before the flop balance."""
+    return (M * p) // P, (M * (p + 1)) // P
+
+
+def rebalance(blk: Block, M_global: int, group=None) -> Block:
+    """Distributed flop-balanced partition: from any contiguous row blocks (e.g. the
+    equal-row blocks each rank read), compute the cuts of `partition_rows` over the
+    global per-row flop without any rank holding the whole matrix, then move rows to
+    their new owners.  Traffic: the global row lengths (4 B per row, all-gathered: the
+    flop of a row needs the lengths of the B rows it names) plus the rows that change
+    owner.  Returns this rank's new block (same contents as `local_block` of the cuts)."""
+    import torch
+    import torch.distributed as dist
+    P = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    dev = blk.col.device
+    rows, _ = _exchange_sizes(blk, group)
+    roff = np.concatenate([[0], np.cumsum(rows)])
+    assert roff[-1] == M_global, "blocks must cover the rows"
+    # 1. global row lengths
+    lens = (blk.ptr[1:] - blk.ptr[:-1]).to(torch.int32)
+    glen = torch.empty(M_global, dtype=torch.int32, device=dev)
+    _p2p_allgatherv(lens, glen, roff, rows, group)
+    # 2. local per-row flop, inclusive prefix, per-rank totals
+    nloc = blk.r1 - blk.r0
+    per = glen.index_select(0, blk.col.long()).to(torch.int64)
+    rid = torch.repeat_interleave(torch.arange(nloc, device=dev), lens.long())
+    f = torch.zeros(nloc, dtype=torch.int64, device=dev).index_add_(0, rid, per)
+    pre = torch.cumsum(f, 0)
+    tot = torch.tensor([int(pre[-1]) if nloc else 0], dtype=torch.int64, device=dev)
+    tots = torch.zeros(P, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(tots, tot, group=group)
+    tots = tots.cpu().numpy()
+    off = int(tots[:me].sum())
+    F = int(tots.sum())
+    # 3. the cuts falling in this rank's prefix range (partition_rows' rule), max-reduced
+    cut = np.zeros(P + 1, np.int64)
+    if F and nloc:
+        gpre = pre.cpu().numpy() + off
+        for q in range(1, P):
+            tgt = F * q / P
+            if off < tgt <= gpre[-1]:
+                cut[q] = blk.r0 + int(np.searchsorted(gpre, tgt, side="left"))
+    cut_t = torch.from_numpy(cut).to(dev)
+    dist.all_reduce(cut_t, op=dist.ReduceOp.MAX, group=group)
+    b = cut_t.cpu().numpy()
+    for q in range(1, P):
+        if not F:
+            b[q] = (M_global * q) // P
+        b[q] = min(max(b[q], b[q - 1]), M_global)
+    b[0], b[P] = 0, M_global
+    # 4. move rows: my [r0, r1) ∩ [b[q], b[q+1]) goes to q, in row order
+    lptr = blk.ptr.cpu().numpy().astype(np.int64)
+    srow = [max(0, min(blk.r1, int(b[q + 1])) - max(blk.r0, int(b[q]))) for q in range(P)]
+    sfirst = [min(max(blk.r0, int(b[q])), blk.r1) - blk.r0 for q in range(P)]
+    snnz = [int(lptr[sfirst[q] + srow[q]] - lptr[sfirst[q]]) if srow[q] else 0 for q in range(P)]
+    cnt = torch.tensor(srow + snnz, dtype=torch.int64, device=dev).view(2, P).t().contiguous().view(-1)
+    cnt_in = torch.zeros(2 * P, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(cnt_in, cnt, group=group)
+    cin = cnt_in.cpu().numpy().reshape(P, 2)
+    rrow, rnnz = cin[:, 0], cin[:, 1]
+    nr, nn = int(b[me + 1] - b[me]), int(rnnz.sum())
+    assert int(rrow.sum()) == nr
+    olen = torch.empty(nr, dtype=torch.int32, device=dev)
+    ocol = torch.empty(nn, dtype=blk.col.dtype, device=dev)
+    oval = torch.empty(nn, dtype=blk.val.dtype, device=dev)
+    ro = np.concatenate([[0], np.cumsum(rrow)])
+    no = np.concatenate([[0], np.cumsum(rnnz)])
+    ops = []
+    for k in range(P):  # self first (a copy), then ring order
+        q_dst, q_src = (me + k) % P, (me - k) % P
+        a0 = sfirst[q_dst]
+        e0 = int(lptr[a0])
+        if q_dst == me:
+            if srow[me]:
+                olen[ro[me]:ro[me + 1]].copy_(lens[a0:a0 + srow[me]])
+                ocol[no[me]:no[me + 1]].copy_(blk.col[e0:e0 + snnz[me]])
+                oval[no[me]:no[me + 1]].copy_(blk.val[e0:e0 + snnz[me]])
+            continue
+        if srow[q_dst]:
+            ops.append(dist.P2POp(dist.isend, lens[a0:a0 + srow[q_dst]].contiguous(), q_dst, group))
+        if snnz[q_dst]:
+            ops.append(dist.P2POp(dist.isend, blk.col[e0:e0 + snnz[q_dst]].contiguous(), q_dst, group))
+            ops.append(dist.P2POp(dist.isend, blk.val[e0:e0 + snnz[q_dst]].contiguous(), q_dst, group))
+        if rrow[q_src]:
+            ops.append(dist.P2POp(dist.irecv, olen[ro[q_src]:ro[q_src + 1]], q_src, group))
+        if rnnz[q_src]:
+            ops.append(dist.P2POp(dist.irecv, ocol[no[q_src]:no[q_src + 1]], q_src, group))
+            ops.append(dist.P2POp(dist.irecv, oval[no[q_src]:no[q_src + 1]], q_src, group))
+    if ops:
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    optr = torch.zeros(nr + 1, dtype=torch.int32, device=dev)
+    torch.cumsum(olen, 0, out=optr[1:])
+    return Block(int(b[me]), int(b[me + 1]), optr, ocol, oval)
 
 
 def _exchange_sizes(blk: Block, group=None):

@@ -139,7 +139,7 @@ def _banded(M=900, width=40, per=8, seed=4):
     return M, ptr.astype(np.int32), c, rng.uniform(0.1, 1.0, len(c))
 
 
-@pytest.mark.parametrize("world,mode", [(2, "halo"), (3, "halo"), (3, "full")])
+@pytest.mark.parametrize("world,mode", [(2, "halo"), (3, "halo"), (3, "full"), (4, "halo"), (4, "full")])
 def test_planned_exchange_gloo(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -175,6 +175,58 @@ def test_rowsharded_allgatherv_gatherv_gloo(world):
     # contiguous cover of the rows
     rows = sorted(o["rows"] for o in out)
     assert rows[0][0] == 0 and all(rows[i][1] == rows[i + 1][0] for i in range(world - 1))
+
+
+def _rebalance_worker(rank, world, port, q):
+    try:
+        sys.path[:0] = [str(ROOT), str(ROOT / "mh-spgemm_amd"), str(ROOT / "tests")]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world))
+        import torch.distributed as dist
+        from mhspgemm import distributed as D
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        res = {"rank": rank}
+        for seed in (3, 8):
+            M, ptr, col, val = _matrix(seed=seed, M=1500)
+            if seed == 8:  # two dense rows hold most of the flop: cuts land on or next to them
+                dense = {100: np.arange(M, dtype=np.int32), 101: np.arange(0, M, 2, dtype=np.int32)}
+                rows = [dense.get(i, col[ptr[i]:ptr[i + 1]]) for i in range(M)]
+                ptr = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+                col = np.concatenate(rows).astype(np.int32)
+                val = np.linspace(0.1, 1.0, len(col))
+            r0, r1 = D.equal_rows(M, world, rank)
+            eq = D.local_block(ptr, col, val, r0, r1, "cpu")
+            nb = D.rebalance(eq, M)
+            bnd = D.partition_rows(D.row_flop(ptr, col, ptr), world)
+            ref = D.local_block(ptr, col, val, int(bnd[rank]), int(bnd[rank + 1]), "cpu")
+            res[f"ok{seed}"] = bool((nb.r0, nb.r1) == (ref.r0, ref.r1) and np.array_equal(nb.ptr.numpy(), ref.ptr.numpy())
+                                    and np.array_equal(nb.col.numpy(), ref.col.numpy())
+                                    and np.array_equal(nb.val.numpy(), ref.val.numpy()))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put(res)
+    except Exception:
+        import traceback
+        q.put({"rank": rank, "error": traceback.format_exc()})
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_rebalance_matches_partition_gloo(world):
+    # the distributed flop balance (each rank starts from an equal-row block, never the
+    # whole matrix) gives every rank exactly the block partition_rows assigns it
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rebalance_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [o["error"] for o in out if "error" in o]
+    assert not errs, errs[0]
+    assert all(o["ok3"] and o["ok8"] for o in out), out
 
 
 def test_partition_balances_flop():

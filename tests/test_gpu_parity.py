@@ -6,6 +6,8 @@ Bar (BASELINE.json north_star): row_ptr and col_idx bit-exact; values within
 mixed-sign values (cancellation) the value tolerance is 1e-6 of the sum of
 |a*b| of the entry, the pattern stays exact (structural zeros are kept).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -471,3 +473,62 @@ def test_hub_rows_span_rank_and_windows(tool, case):
                      rng.uniform(0.1, 1.0, int(Ap[-1])))
     t = check(tool, A, B)
     assert t.num_bins[4] >= 6, t.num_bins  # the hub rows run in the 1024-thread kernel
+
+
+def test_oom_row_chunked_fallback(tool):
+    # SURVEY §5 fallback: a context whose memory budget holds C but not C beside the full
+    # workspace runs the product row-chunked (workspace for a quarter of the rows here);
+    # the result is the same C
+    from mhspgemm import _lib as L
+    A = synth.cant_like()
+    A.H2D(tool.device)
+    small = mhspgemm.Tool(tool.device)
+    try:
+        small.set_option(L.MHS_OPT_MEM_BUDGET, 300)  # MiB: C is 210 MB, the full workspace ~170 MB
+        C, t = mhspgemm.spgemm(small, A, A)
+        p, c, v = C.to_host()
+        C.release()
+        assert small.chunked_calls() == 1
+        Cp, Ci, Cv = orc.spgemm(A.ptr, A.col, A.val, A.ptr, A.col, A.val, A.N)
+        assert np.array_equal(p, Cp) and np.array_equal(c, Ci)
+        assert mhspgemm.compare_tol(Cp, Ci, Cv, p, c, v, RTOL, ATOL)[0]
+        assert t.nnzC == Cp[-1] and t.flop == orc.flop(A.col, A.ptr)
+        # C alone beyond the budget: MHS_ERR_OOM after the chunked retry
+        small.set_option(L.MHS_OPT_MEM_BUDGET, 150)
+        with pytest.raises(mhspgemm.MHSpGEMMError) as e:
+            mhspgemm.spgemm(small, A, A)
+        assert e.value.status == 2
+    finally:
+        small.close()
+
+
+def test_probe_conflict_counter():
+    # the reference's HASH_CONFLICT diagnostic (inc/common.h:18, src/main.cu:68-71): the probe
+    # build counts conflicts of the hashed tile tables; the product library refuses the query
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "import mhspgemm\n"
+        "from mhspgemm import synth\n"
+        "A = synth.SYNTH['cop20k_A']()\n"
+        "A.H2D(0)\n"
+        "t = mhspgemm.Tool(0)\n"
+        "try:\n"
+        "    t.probe_conflicts()\n"
+        "except mhspgemm.MHSpGEMMError as e:\n"
+        "    print('REFUSED', e.status)\n"
+        "C, _ = mhspgemm.spgemm(t, A, A); C.release()\n"
+        "print('CONFLICTS', t.probe_conflicts(), t.probe_conflicts())\n"
+    ) % (str(root), str(root / "mh-spgemm_amd"))
+    env = dict(os.environ)
+    env["MHS_LIB"] = str(root / "mh-spgemm_amd" / "mhspgemm" / "libmhspgemm_probe.so")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("CONFLICTS")][0].split()
+    assert int(line[1]) > 0 and int(line[2]) == 0, line  # counted, then reset by the query
+    env.pop("MHS_LIB")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert "REFUSED 3" in out.stdout, out.stdout + out.stderr[-2000:]
