@@ -121,6 +121,7 @@ struct Stats {
     int sym_count[NBINS];
     int num_count[NBINS];
     int num_global_need;           // max LDS-equivalent bytes of a global numeric row
+    int num_block_need[2];         // max LDS bytes of a row in NUM_B256 / NUM_B1024 (launch sizing)
     int final_done;                // k_scan_final blocks finished (last one publishes)
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric

@@ -198,6 +198,7 @@ __device__ __forceinline__ int hslot(int key, int H) {
 __device__ __forceinline__ int hnext(int s, int H) { return s + 1 < H ? s + 1 : 0; }
 
 __device__ __forceinline__ int sat_int(long long x) { return x > INT_MAX ? INT_MAX : (int)x; }
+__device__ __forceinline__ int hi_lo_span(int lo, int hi) { return hi - lo + 1; }
 
 // Streaming accesses (C, the symbolic -> numeric row cache): each byte is written or read
 // once, so they bypass L2 allocation (nontemporal) and leave the XCD's 4 MiB to the B rows
@@ -238,16 +239,22 @@ __device__ __forceinline__ T ld_cache(const T* p) {
 // ceil(nA / groups) * ceil(avg B-row length / G) (ties -> wider, better
 // coalesced groups); at most 64 groups so one staged chunk of 64 A entries
 // feeds every group.
-__device__ __forceinline__ int pick_group(long long work, int nA, int T, int gfloor = 4) {
+#ifndef MHS_PICK_U
+#define MHS_PICK_U 1  // count load batches of U entries per lane in the sweep cost (0: entries)
+#endif
+__device__ __forceinline__ int pick_group(long long work, int nA, int T, int gfloor = 4, int unroll = 1) {
     int gmin = T / 64;
     if (gmin < gfloor) gmin = gfloor;
     if (nA <= 0) return gmin;
     const long long avg = (work + nA - 1) / nA;
+    const int U = MHS_PICK_U ? unroll : 1;
     int best = gmin;
     long long bc = LLONG_MAX;
     for (int g = gmin; g <= T; g <<= 1) {
         const int ng = T / g;
-        const long long c = (long long)((nA + ng - 1) / ng) * ((avg + g - 1) / g);
+        // sweeps = A entries per group x load batches per entry (a batch: U entries per lane,
+        // issued together -- one dependent round trip)
+        const long long c = (long long)((nA + ng - 1) / ng) * ((avg + (long long)g * U - 1) / ((long long)g * U));
         if (c <= bc) {
             bc = c;
             best = g;
@@ -1336,10 +1343,12 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
         // (a staged round chains A entry -> bmeta -> B load round trips behind two barriers
         // per 64*STAGE_SUBS entries)
         wave_chunks(a0 + 64 * (tm.rank() >> 6), Team::size, a1, Acol, Aval, bmeta, tiles,
-                    pick_group(work, nA, 64, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN), f);
+                    pick_group(work, nA, 64, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN, tiles ? 1 : MHS_UNROLL), f);
     else
         for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
-                     pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN), f, stage);
+                     pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN,
+                                tiles ? 1 : MHS_UNROLL),  // (tile walks: measured better by entries)
+                     f, stage);
 }
 
 // ---------------------------------------------------------- tile tables ---
@@ -2058,6 +2067,19 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                   tok);
         }
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
+        // the block kernels' launches get the LDS their largest row needs (more blocks per
+        // CU than a fixed 64 / 157 KiB when the rows are smaller)
+        int need = 0;
+        if (nbin == NUM_B256 || nbin == NUM_B1024) {
+            const int span = hi_lo_span(rlo[i], rhi[i]);
+            const int t = ctiles[i], n = v[k];
+            need = nbin == NUM_B1024 && num_wide(span, t, n, dense_span_max)     ? B1024_BYTES
+                   : nbin == NUM_B1024 && num_ranked(span, t, n, dense_span_max) ? (int)num_need_ranked(span, t, n)
+                                                                                 : (int)num_need(span, t, n, dense_span_max);
+        }
+        const int n256 = wave_max(nbin == NUM_B256 ? need : 0), n1024 = wave_max(nbin == NUM_B1024 ? need : 0);
+        if (lane == 0 && n256) atomicMax(&stats->num_block_need[0], n256);
+        if (lane == 0 && n1024) atomicMax(&stats->num_block_need[1], n1024);
     }
     __syncthreads();
     if (w == 0) {
@@ -3107,6 +3129,17 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
                        w.blkflop, w.nflop);
 }
 
+// Dynamic LDS of a block-kernel launch: the header plus its largest row's tables, in
+// 2 KiB steps, at most the bin's budget (MHS_BLOCK_LDS_FIXED=1: always the budget).
+#ifndef MHS_BLOCK_LDS_FIXED
+#define MHS_BLOCK_LDS_FIXED 0
+#endif
+static int block_lds(int need, int budget) {
+    if (MHS_BLOCK_LDS_FIXED || need <= 0) return budget;
+    const int b = (BLOCK_HDR + need + 2047) & ~2047;
+    return b < budget ? b : budget;
+}
+
 int numeric_launches(const Stats& h) {
     int n = 0, small = 0;
     for (int b = 1; b < NUM_NB; ++b) {
@@ -3172,14 +3205,16 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         a.list = w.bin_list + (long long)(NUM_B1024 - 1) * A.M;
         a.cursor = w.cursors + NUM_B1024 * 8 * CURSOR_STRIDE;
         s = next_stream();
-        hipLaunchKernelGGL((k_num_block<1024, false>), dim3(round8(count, 256)), dim3(1024), LDS_MAX - 1024, s, a);
+        hipLaunchKernelGGL((k_num_block<1024, false>), dim3(round8(count, 256)), dim3(1024),
+                           block_lds(h.num_block_need[1], LDS_MAX - 1024), s, a);
     }
     if (h.num_count[NUM_B256] > 0) {
         const int count = a.count = h.num_count[NUM_B256];
         a.list = w.bin_list + (long long)(NUM_B256 - 1) * A.M;
         a.cursor = w.cursors + NUM_B256 * 8 * CURSOR_STRIDE;
         s = next_stream();
-        hipLaunchKernelGGL((k_num_block<256, false>), dim3(round8(count, 1024)), dim3(256), NUM_B256_BYTES, s, a);
+        hipLaunchKernelGGL((k_num_block<256, false>), dim3(round8(count, 1024)), dim3(256),
+                           block_lds(h.num_block_need[0], NUM_B256_BYTES), s, a);
     }
     if (h.num_count[NUM_W16H] > 0) {
         const int count = a.count = h.num_count[NUM_W16H];
