@@ -48,6 +48,9 @@
 #ifndef MHS_UNROLL
 #define MHS_UNROLL 4  // B entries per lane issued together in the product walk
 #endif
+#ifndef MHS_UNROLL_BLOCK
+#define MHS_UNROLL_BLOCK 8  // ... in the block kernels (measured: S1-like rows -9%; the wave kernels keep 4)
+#endif
 #ifndef MHS_NUM_WS_GRID
 #define MHS_NUM_WS_GRID 4096  // block cap of the small-row numeric launch
 #endif
@@ -853,10 +856,10 @@ __device__ __forceinline__ void run_segment(const F& f, int s, int n, int gl, in
 // Value walk over one run of LM (compile-time bound) B rows, L (<= LM) of them
 // live: B entry q of row k+i is s + i*n + q.  Loads of dead rows are clamped to
 // row k (a cache hit) rather than branched around.
-template <int LM, class F>
+template <int LM, int UV = MHS_UNROLL, class F>
 __device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl, int G,
                                                 const double (&a)[LM], int L) {
-    constexpr int U = LM == 1 ? MHS_UNROLL : MHS_RUN_UNROLL;
+    constexpr int U = LM == 1 ? UV : MHS_RUN_UNROLL;
     int o[LM];
 #pragma unroll
     for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
@@ -1180,7 +1183,7 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
                 if constexpr (F::kValues) {
                     if (lmax == 1) {
                         const double a[1] = {Aval[v.z]};
-                        run_segment_run<1>(f, v.x, v.y, gl, G, a, 1);
+                        run_segment_run<1, MHS_UNROLL_BLOCK>(f, v.x, v.y, gl, G, a, 1);
                     } else if (lmax == 2) {
                         const double a[2] = {Aval[v.z], Aval[v.z + (v.w > 1)]};
                         run_segment_run<2>(f, v.x, v.y, gl, G, a, v.w);
@@ -1347,7 +1350,7 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
     else
         for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
                      pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN,
-                                tiles ? 1 : MHS_UNROLL),  // (tile walks: measured better by entries)
+                                tiles ? 1 : (Team::size > 64 ? MHS_UNROLL_BLOCK : MHS_UNROLL)),  // (tile walks: by entries)
                      f, stage);
 }
 
