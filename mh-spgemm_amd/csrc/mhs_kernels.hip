@@ -487,6 +487,110 @@ __device__ void team_bitonic(const Team& tm, unsigned long long* S, int P) {
     }
 }
 
+// Lane exchange v <- lane ^ d (d a power of two, a compile-time constant once the
+// callers' loops are unrolled) without the LDS crossbar where the hardware has a path:
+// DPP quad_perm for d = 1, 2; DPP row shifts + select for d = 4, 8 (both neighbours are
+// inside the lane's 16-lane row); ds_swizzle (xor mode, no LDS memory access) for 16;
+// ds_bpermute only for 32.  Every lane of the wave must be active.
+#ifndef MHS_DPP
+#define MHS_DPP 1
+#endif
+__device__ __forceinline__ int xor_lanes(int v, int d) {
+    if (MHS_DPP) {
+        const int lane = lane_id();
+        if (d == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        if (d == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+        if (d == 4) {
+            const int up = __builtin_amdgcn_mov_dpp(v, 0x104, 0xF, 0xF, false);  // row_shl:4  (lane + 4)
+            const int dn = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4  (lane - 4)
+            return (lane & 4) ? dn : up;
+        }
+        if (d == 8) {
+            const int up = __builtin_amdgcn_mov_dpp(v, 0x108, 0xF, 0xF, false);  // row_shl:8
+            const int dn = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
+            return (lane & 8) ? dn : up;
+        }
+        if (d == 16) return __builtin_amdgcn_ds_swizzle(v, 0x401F);  // and 0x1F, xor 0x10
+    }
+    return __shfl_xor(v, d);
+}
+
+// DPP row shift right by d (d in 1, 2, 4, 8; lanes whose source is outside their 16-lane row
+// read 0), whole-wave shifts by one lane, row broadcasts (GFX9 row_bcast:15 / :31).
+__device__ __forceinline__ int row_shr(int v, int d) {
+    if (d == 1) return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+    if (d == 2) return __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+    if (d == 4) return __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+    return __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+}
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int wave_shl1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, true); }
+template <int ROWS>
+__device__ __forceinline__ int row_bcast15(int v) {  // lane 15 of row r -> row r+1 (rows in ROWS), else 0
+    return __builtin_amdgcn_update_dpp(0, v, 0x142, ROWS, 0xF, false);
+}
+template <int ROWS>
+__device__ __forceinline__ int row_bcast31(int v) {  // lane 31 -> rows 2, 3 (in ROWS), else 0
+    return __builtin_amdgcn_update_dpp(0, v, 0x143, ROWS, 0xF, false);
+}
+// Inclusive scan over teams of W lanes (aligned groups of W consecutive lanes).
+template <int W>
+__device__ __forceinline__ int team_incl_scan(int x, int tl) {
+    if (!MHS_DPP) {
+#pragma unroll
+        for (int d = 1; d < W; d <<= 1) {
+            const int o = __shfl_up(x, d, W);
+            x += tl >= d ? o : 0;
+        }
+        return x;
+    }
+#pragma unroll
+    for (int d = 1; d < (W < 16 ? W : 16); d <<= 1) {
+        const int o = row_shr(x, d);
+        x += tl >= d ? o : 0;  // (W < 16: teams share a row -- the guard keeps them apart)
+    }
+    if (W >= 32) x += row_bcast15<0xA>(x);
+    if (W == 64) x += row_bcast31<0xC>(x);
+    return x;
+}
+
+// Segmented inclusive sum over teams of W lanes: a lane with `seen` set starts a segment.
+template <int W>
+__device__ __forceinline__ double team_seg_scan(double sum, bool seen, int tl) {
+    if (!MHS_DPP) {
+#pragma unroll
+        for (int d = 1; d < W; d <<= 1) {
+            const double os = __shfl_up(sum, d, W);
+            const int of = __shfl_up((int)seen, d, W);
+            const bool add = tl >= d && !seen;
+            sum += add ? os : 0.0;
+            seen = add ? of != 0 : seen;
+        }
+        return sum;
+    }
+#pragma unroll
+    for (int d = 1; d < (W < 16 ? W : 16); d <<= 1) {
+        const int oh = row_shr(__double2hiint(sum), d), ol = row_shr(__double2loint(sum), d);
+        const int of = row_shr((int)seen, d);
+        const bool add = tl >= d && !seen;
+        sum += add ? __hiloint2double(oh, ol) : 0.0;
+        seen = add ? of != 0 : seen;
+    }
+    auto carry = [&](int oh, int ol, bool rows) {
+        if (rows && !seen) sum += __hiloint2double(oh, ol);
+    };
+    const int row = lane_id() >> 4;
+    if (W == 32) {  // rows 1, 3 take lane 15 / 47 of the row below
+        carry(row_bcast15<0xA>(__double2hiint(sum)), row_bcast15<0xA>(__double2loint(sum)), (row & 1) != 0);
+    } else if (W == 64) {  // row 1 <- lane 15, then row 2 <- lane 31, then row 3 <- lane 47 (each
+                           // already final: a lane without a head in its row continues the row below)
+        carry(row_bcast15<0x2>(__double2hiint(sum)), row_bcast15<0x2>(__double2loint(sum)), row == 1);
+        carry(row_bcast31<0x4>(__double2hiint(sum)), row_bcast31<0x4>(__double2loint(sum)), row == 2);
+        carry(row_bcast15<0x8>(__double2hiint(sum)), row_bcast15<0x8>(__double2loint(sum)), row == 3);
+    }
+    return sum;
+}
+
 // Bitonic sort of W*K unsigned keys held by a team of W lanes, K per lane, ascending
 // over element e = i*W + tl (slot i, team lane tl): partners at distance d < W are in
 // other lanes (shuffles), at d >= W in other slots of the lane.  Compare-exchange by
@@ -500,7 +604,7 @@ __device__ __forceinline__ void reg_bitonic(unsigned (&key)[K], int tl) {
             if (d < W) {
                 unsigned ok[K];
 #pragma unroll
-                for (int i = 0; i < K; ++i) ok[i] = (unsigned)__shfl_xor((int)key[i], d, W);
+                for (int i = 0; i < K; ++i) ok[i] = (unsigned)xor_lanes((int)key[i], d);  // d < W: inside the team
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
                     const bool asc = ((i * W + tl) & k) == 0, low = (tl & d) == 0;
@@ -2768,12 +2872,7 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
             len = m.y;
             if (NUMERIC) av = a.Aval[a0 + tl];
         }
-        int incl = len;  // inclusive scan of the B-row lengths over the team
-#pragma unroll
-        for (int d = 1; d < W; d <<= 1) {
-            const int o = __shfl_up(incl, d, W);
-            incl += tl >= d ? o : 0;
-        }
+        const int incl = team_incl_scan<W>(len, tl);  // inclusive scan of the B-row lengths over the team
         const int flop = __shfl(incl, tb + W - 1);
         const int excl = incl - len;
         // sort keys: symbolic the column; numeric (column << TINY_EBITS) | element, the
@@ -2854,16 +2953,9 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
             int rank0 = 0;       // heads in slots < i
 #pragma unroll
             for (int i = 0; i < K; ++i) {
-                double sum = v[i];
-                bool seen = head[i];
-#pragma unroll
-                for (int d = 1; d < W; d <<= 1) {
-                    const double os = __shfl_up(sum, d, W);
-                    const int of = __shfl_up((int)seen, d, W);
-                    const bool add = tl >= d && !seen;
-                    sum += add ? os : 0.0;
-                    seen = add ? of != 0 : seen;
-                }
+                // the lane's segment began in this slot iff a head sits at or below it in the team
+                const bool seen = (__ballot(head[i]) & tmask & (below | (1ull << lane))) != 0;
+                double sum = team_seg_scan<W>(v[i], head[i], tl);
                 sum += seen ? 0.0 : carry;  // the segment began in an earlier slot
                 const int nc = __shfl_down(c[i], 1, W);
                 const int nxt = i + 1 < K ? __shfl(c[i + 1 < K ? i + 1 : i], tb) : INT_MAX;
