@@ -39,12 +39,31 @@ constexpr int CURSOR_INTS = CURSOR_SLOTS * 8 * CURSOR_STRIDE;
 // Tiny rows: a team of W lanes per row holding K products per lane (flop <= W*K,
 // nA <= W), sorted by column in registers -- no table (numeric parks the values in
 // LDS by element during the sort).  Classes, smallest first; a row takes the first
-// class it fits: (8,1) (32,1) (32,2) (32,4) (64,4) (64,8).
+// class it fits (tiny_w / tiny_k below).
 constexpr int TINY_NC = 6;
 constexpr int TINY_EBITS = 9;              // numeric sort key = (column << 9) | element (W*K <= 512)
 constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so a numeric tiny row spans < 2^23 columns (offsets from its first tile)
+// Classes of the two phases (measured per phase on delaunay-, GAP-road-, mac_econ-like):
+// symbolic (counts only: no segmented sums) sorts every row of at most 8 A entries in
+// 8-lane teams -- eight rows per wave, so one dependent load chain (row -> A -> bmeta -> B)
+// serves eight rows: (8,1) (8,4) (8,8) (32,4).  Numeric keeps its values beside the keys
+// and sums segments per slot, so wide slots cost more: (8,1) (8,4) (32,2) (32,4) (64,4) (64,8).
+// MHS_TINY_SET=0: round 1's classes (8,1) (32,1) (32,2) (32,4) (64,4) (64,8) for both.
+#ifndef MHS_TINY_SET
+#define MHS_TINY_SET 1
+#endif
+#if MHS_TINY_SET
+__host__ __device__ constexpr int tiny_w(int c) { return c <= 1 ? 8 : c <= 3 ? 32 : 64; }
+__host__ __device__ constexpr int tiny_k(int c) { return c == 0 ? 1 : c == 2 ? 2 : c == 5 ? 8 : 4; }
+__host__ __device__ constexpr int tiny_ws(int c) { return c <= 2 ? 8 : 32; }
+__host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? 1 : c == 2 ? 8 : 4; }
+#else
 __host__ __device__ constexpr int tiny_w(int c) { return c == 0 ? 8 : c <= 3 ? 32 : 64; }
 __host__ __device__ constexpr int tiny_k(int c) { return c <= 1 ? 1 : c == 2 ? 2 : c <= 4 ? 4 : 8; }
+__host__ __device__ constexpr int tiny_ws(int c) { return tiny_w(c); }
+__host__ __device__ constexpr int tiny_ks(int c) { return tiny_k(c); }
+#endif
+constexpr int TINY_FUSED_KMAX = 4;  // largest K of the numeric classes 0..3 (one fused launch)
 // Symbolic uses the classes below TINY_SYM_NC only (past 128 products a hash table
 // counts faster than a sort); numeric uses the 64-lane classes for rows whose table
 // would not fit the small wave bin (measured: cop20k-like 2.3x slower sorted, while
@@ -58,6 +77,12 @@ __host__ __device__ inline int tiny_class(int flop, int nA, int nc = TINY_NC) {
     if (flop <= 0) return -1;
     for (int c = 0; c < nc; ++c)
         if (flop <= tiny_w(c) * tiny_k(c) && nA <= tiny_w(c)) return c;
+    return -1;
+}
+__host__ __device__ inline int tiny_class_sym(int flop, int nA) {
+    if (flop <= 0) return -1;
+    for (int c = 0; c < 4; ++c)
+        if (flop <= tiny_ws(c) * tiny_ks(c) && nA <= tiny_ws(c)) return c;
     return -1;
 }
 enum SymBin : int {

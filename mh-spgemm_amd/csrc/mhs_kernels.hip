@@ -857,7 +857,7 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         rlo[row] = lo;
         rhi[row] = hi;
         const int nA = Aptr[row + 1] - Aptr[row];
-        const int tc = tiny_class(f, nA, TINY_SYM_NC);
+        const int tc = tiny_class_sym(f, nA);
         const int bin = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
         if (bin == SYM_NONE) {
@@ -2299,7 +2299,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     MHS_STAMP(0);
     // symbolic kept the masks unless it sorted the row as a tiny one (numeric runs those
     // with tables when the tiny classes are off: N beyond the packed keys' 23 bits)
-    const bool sym_tiny = tiny_class(__builtin_amdgcn_readfirstlane(a.rflop[row]), a1 - a0, TINY_SYM_NC) >= 0;
+    const bool sym_tiny = tiny_class_sym(__builtin_amdgcn_readfirstlane(a.rflop[row]), a1 - a0) >= 0;
     // hashed rows rank their tiles by a bitmap over the span (block teams / many tiles,
     // when it fits the accumulator), else by counting (few tiles), else by a sort
     const bool rank_bitmap = MODE == NM_HASH && (Team::size > 64 || t >= 64) &&
@@ -2995,10 +2995,10 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(8) void k_tiny_num_small(TinyArgs
     a.bin = NUM_TINY + f.c[k];
     a.list += (long long)(a.bin - 1) * a.M;
     switch (f.c[k]) {
-    case 0: tiny_rows<8, 1, true>(a, bid, nb); break;
-    case 1: tiny_rows<32, 1, true>(a, bid, nb); break;
-    case 2: tiny_rows<32, 2, true>(a, bid, nb); break;
-    default: tiny_rows<32, 4, true>(a, bid, nb); break;
+    case 0: tiny_rows<tiny_w(0), tiny_k(0), true>(a, bid, nb); break;
+    case 1: tiny_rows<tiny_w(1), tiny_k(1), true>(a, bid, nb); break;
+    case 2: tiny_rows<tiny_w(2), tiny_k(2), true>(a, bid, nb); break;
+    default: tiny_rows<tiny_w(3), tiny_k(3), true>(a, bid, nb); break;
     }
 }
 
@@ -3007,17 +3007,16 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(8) void k_tiny_num_small(TinyArgs
 constexpr int TINY_SYM_GRID = 1024;
 __device__ __forceinline__ void tiny_sym_rows(TinyArgs a, int blk) {
     const int c = blk / TINY_SYM_GRID, bid = blk % TINY_SYM_GRID;
-    static_assert(TINY_NC == 6 && tiny_w(0) == 8 && tiny_k(0) == 1 && tiny_w(1) == 32 && tiny_k(1) == 1 &&
-                      tiny_w(2) == 32 && tiny_k(2) == 2 && tiny_w(3) == 32 && tiny_k(3) == 4 &&
-                      tiny_w(4) == 64 && tiny_k(4) == 4 && tiny_w(5) == 64 && tiny_k(5) == 8 && TINY_SYM_NC == 4,
+    static_assert(TINY_NC == 6 && TINY_SYM_NC == 4 && tiny_ws(3) <= 32 && tiny_w(3) <= 32 && tiny_w(4) == 64 &&
+                      tiny_w(5) == 64,
                   "k_tiny_sym / launch_tiny_num instantiate the classes of tiny_class()");
     a.bin = SYM_TINY + c;
     a.list += (long long)c * a.M;
     switch (c) {
-    case 0: tiny_rows<8, 1, false>(a, bid, TINY_SYM_GRID); break;
-    case 1: tiny_rows<32, 1, false>(a, bid, TINY_SYM_GRID); break;
-    case 2: tiny_rows<32, 2, false>(a, bid, TINY_SYM_GRID); break;
-    default: tiny_rows<32, 4, false>(a, bid, TINY_SYM_GRID); break;
+    case 0: tiny_rows<tiny_ws(0), tiny_ks(0), false>(a, bid, TINY_SYM_GRID); break;
+    case 1: tiny_rows<tiny_ws(1), tiny_ks(1), false>(a, bid, TINY_SYM_GRID); break;
+    case 2: tiny_rows<tiny_ws(2), tiny_ks(2), false>(a, bid, TINY_SYM_GRID); break;
+    default: tiny_rows<tiny_ws(3), tiny_ks(3), false>(a, bid, TINY_SYM_GRID); break;
     }
 }
 
@@ -3147,12 +3146,12 @@ static void launch_tiny_num(int c, int rows, const TinyArgs& t, hipStream_t s) {
     hipLaunchKernelGGL((k_tiny_num<WW, KK>), dim3(round8((rows + 256 / (WW) - 1) / (256 / (WW)), 4096)), \
                        dim3(256), 256 * (KK) * 8, s, t)
     switch (c) {
-    case 0: MHS_TINY(8, 1); break;
-    case 1: MHS_TINY(32, 1); break;
-    case 2: MHS_TINY(32, 2); break;
-    case 3: MHS_TINY(32, 4); break;
-    case 4: MHS_TINY(64, 4); break;
-    default: MHS_TINY(64, 8); break;
+    case 0: MHS_TINY(tiny_w(0), tiny_k(0)); break;
+    case 1: MHS_TINY(tiny_w(1), tiny_k(1)); break;
+    case 2: MHS_TINY(tiny_w(2), tiny_k(2)); break;
+    case 3: MHS_TINY(tiny_w(3), tiny_k(3)); break;
+    case 4: MHS_TINY(tiny_w(4), tiny_k(4)); break;
+    default: MHS_TINY(tiny_w(5), tiny_k(5)); break;
     }
 #undef MHS_TINY
 }
@@ -3358,7 +3357,9 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             launch_tiny_num(c, count, tc, next_stream());
         }
         TinyFused f{};
-        static_assert(tiny_w(3) == 32 && tiny_k(3) == 4 && tiny_w(4) == 64, "classes 0..3 fuse (W <= 32, K <= 4)");
+        static_assert(tiny_w(3) <= 32 && tiny_k(0) <= TINY_FUSED_KMAX && tiny_k(1) <= TINY_FUSED_KMAX &&
+                          tiny_k(2) <= TINY_FUSED_KMAX && tiny_k(3) <= TINY_FUSED_KMAX && tiny_w(4) == 64,
+                      "classes 0..3 fuse (W <= 32, K <= TINY_FUSED_KMAX)");
         for (int c = 3; c >= 0; --c) {
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;
@@ -3371,7 +3372,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         if (f.nclass > 0) {
             t.list = w.bin_list;
             s = next_stream();
-            hipLaunchKernelGGL(k_tiny_num_small, dim3(f.blk0[f.nclass]), dim3(256), 256 * 4 * 8, s, t, f);
+            hipLaunchKernelGGL(k_tiny_num_small, dim3(f.blk0[f.nclass]), dim3(256), 256 * TINY_FUSED_KMAX * 8, s, t, f);
         }
     }
     if (h.num_count[NUM_W16G] > 0) {

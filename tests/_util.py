@@ -194,8 +194,8 @@ def group_zoo(seed: int = 3, K: int = 6000, N: int = 30_000):
 
 
 def tiny_zoo(seed: int = 7, K: int = 3000, N: int = 5000):
-    """Rows for every tiny class (team of W lanes x K products per lane: flop <= 8 with
-    nA <= 8; <= 32, 64, 128 with nA <= 32; <= 256, 512 with nA <= 64), with colliding
+    """Rows for every tiny class (team of W lanes x K products per lane: flop <= 8, 32, 64
+    with nA <= 8; <= 32, 64, 128 with nA <= 32; <= 256, 512 with nA <= 64), with colliding
     columns (B rows drawn from a narrow column window, repeated A entries) so segments of
     equal columns span lanes and slots, plus rows just past the limits (flop 513+, nA
     past the lane count with empty B rows)."""
@@ -217,7 +217,8 @@ def tiny_zoo(seed: int = 7, K: int = 3000, N: int = 5000):
     nonempty = np.nonzero(blen)[0]
     empty = np.nonzero(blen == 0)[0]
     arows = []
-    for target, amax in ((1, 8), (4, 8), (8, 8), (20, 32), (32, 32), (50, 32), (64, 32), (100, 32), (128, 32),
+    for target, amax in ((1, 8), (4, 8), (8, 8), (16, 8), (30, 8), (32, 8), (60, 8), (64, 8), (20, 32), (32, 32),
+                         (50, 32), (64, 32), (100, 32), (128, 32),
                          (129, 32), (200, 64), (256, 64), (300, 64), (512, 64), (513, 64), (700, 64)):
         for _ in range(30):
             ks, f = [], 0
