@@ -27,7 +27,10 @@ constexpr int TILE_BITS = 64;
 constexpr int NBINS = 16;  // capacity of the per-bin counters
 constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
 constexpr int LDS_MAX_C = 163840;  // gfx950: 160 KiB per workgroup (probed on the box)
-constexpr int SCAN_ITEMS = 1024;// rows per block in the row_ptr scan and the bin-list passes
+#ifndef MHS_SCAN_ITEMS
+#define MHS_SCAN_ITEMS 1024
+#endif
+constexpr int SCAN_ITEMS = MHS_SCAN_ITEMS;  // rows per block (of 1024 threads) in the row_ptr scan and the bin lists
 // Row cursors of the dynamically scheduled bin walks: a launch slot (numeric bin b: b,
 // symbolic bin b: NUM_NB + b) has one cursor per XCD group, 64 bytes apart.  They live after
 // k_scan's look-back words and are zeroed with them by k_analyze.

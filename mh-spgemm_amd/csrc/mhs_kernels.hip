@@ -1983,10 +1983,10 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
 // binof[j]) to contiguous per-bin lists: bin x's rows at list + (x-1)*M, cursor
 // cnt[x].  The block's rows keep row order; one atomic per (block, bin) reserves
 // their places (the grids that call this have M/4096 blocks: little contention).
-template <int NB>
+template <int NB, int PER>
 __device__ void append_block_rows(const unsigned char* binof, long long M, int* __restrict__ cnt,
                                   int* __restrict__ list, int blk) {
-    constexpr int PER = SCAN_ITEMS / 1024;
+    constexpr int ITEMS = 1024 * PER;
     static_assert(PER * 16 <= 64 && NB <= 16, "one wave scans one bin's (pass, wave) counts");
     __shared__ int wc[NB][PER * 16];  // [bin][pass*16 + wave]: members, then exclusive prefix
     __shared__ int nbase[NB];
@@ -2015,7 +2015,7 @@ __device__ void append_block_rows(const unsigned char* binof, long long M, int* 
         const int x = mybin[k];
         if (x > 0)
             list[(long long)(x - 1) * M + nbase[x] + wc[x][k * 16 + w] + rank[k]] =
-                blk * SCAN_ITEMS + k * 1024 + threadIdx.x;
+                blk * ITEMS + k * 1024 + threadIdx.x;
     }
 }
 
@@ -2024,13 +2024,14 @@ __device__ void append_block_rows(const unsigned char* binof, long long M, int* 
 // of same-pattern rows containing it, broken every RG_BREAK rows, cut into groups of
 // RG_MAX from the run start.  Only group heads enter the symbolic lists (a group's
 // rows share one C pattern).
+template <int PER>
 __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* __restrict__ bin_id,
                                                    const unsigned char* __restrict__ asame,
                                                    unsigned char* __restrict__ grp, int groups,
                                                    int* __restrict__ cnt, int* __restrict__ list) {
-    __shared__ unsigned char binof[SCAN_ITEMS];
-    for (int j = threadIdx.x; j < SCAN_ITEMS; j += 1024) {
-        const long long i = (long long)blockIdx.x * SCAN_ITEMS + j;
+    __shared__ unsigned char binof[1024 * PER];
+    for (int j = threadIdx.x; j < 1024 * PER; j += 1024) {
+        const long long i = (long long)blockIdx.x * (1024 * PER) + j;
         unsigned char b = 0;
         if (i < M) {
             int g = 1;
@@ -2050,7 +2051,7 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
         binof[j] = b;
     }
     __syncthreads();
-    append_block_rows<SYM_NB>(binof, M, cnt, list, (int)blockIdx.x);
+    append_block_rows<SYM_NB, PER>(binof, M, cnt, list, (int)blockIdx.x);
 }
 
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
@@ -2092,6 +2093,7 @@ __device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t
 // publishes Stats to the host.
 constexpr int SCAN_TICKET_MIN = 256;  // k_scan grids above this take dispatch-order tickets
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+template <int PER>
 __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                unsigned long long* __restrict__ state,
                                                const int* __restrict__ rflop,
@@ -2103,8 +2105,8 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                int* __restrict__ list, Stats* __restrict__ stats,
                                                int dense_span_max, Published* pub, int seq, int tiny_ok,
                                                const unsigned long long* __restrict__ blkflop, int nflop) {
-    static_assert(SCAN_ITEMS == 1024, "one item per thread");
-    constexpr int PER = 1;
+    constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
+    static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
     __shared__ long long excl_s;
     __shared__ int bid_s;
@@ -2118,7 +2120,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         __syncthreads();
         bid = bid_s;
     }
-    const int base = bid * SCAN_ITEMS + threadIdx.x * PER;
+    const int base = bid * ITEMS + threadIdx.x * PER;
     int v[PER];
     long long loc = 0;
 #pragma unroll
@@ -2150,7 +2152,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     }
     // numeric bin of every row (independent of the prefix: its loads overlap the
     // predecessors' publication instead of following the look-back)
-    __shared__ unsigned char nbin_of[SCAN_ITEMS];
+    __shared__ unsigned char nbin_of[ITEMS];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = base + k;
@@ -2237,7 +2239,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         off += v[k];
     }
     __syncthreads();
-    append_block_rows<NUM_NB>(nbin_of, M, stats->num_count, list, bid);
+    append_block_rows<NUM_NB, PER>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
     if (pub) {
         publish_stats(stats, pub, seq);
@@ -3033,9 +3035,21 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_common(Sy
 
 // -------------------------------------------------------------- launchers ---
 
+// Rows per block of the row_ptr scan and the bin lists: 4096 (four per thread) for big
+// matrices -- a quarter of the blocks, so a quarter of the per-(block, bin) cursor atomics
+// (tiny-row matrices of millions of rows were bound by them) -- 1024 below, where fewer
+// blocks would leave the chip idle (measured: cant-like -6% at 4096).
+#ifndef MHS_SCAN_BIG_M
+#define MHS_SCAN_BIG_M (1 << 19)
+#endif
+static int scan_per(int M) { return M >= MHS_SCAN_BIG_M ? 4 : 1; }
+
+#ifndef MHS_ROW_GMIN
+#define MHS_ROW_GMIN 4  // narrowest lane group per row in k_mask_b / k_analyze (tiny rows: 16 per wave)
+#endif
 static int pick_group(long long nnz, int rows, int gmax = 64) {
     const long long avg = rows > 0 ? (nnz + rows - 1) / rows : 1;
-    int g = 8;
+    int g = MHS_ROW_GMIN;
     while (g < avg && g < gmax) g <<= 1;
     return g;
 }
@@ -3051,11 +3065,12 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     // about four chunk iterations per row: a wave then holds several rows, whose
     // dependent load chains overlap (measured on gfx950: 64-lane rows were latency-bound)
     const long long avg = B.M > 0 ? B.nnz / B.M : 0;
-    int G = 8;
+    int G = avg < 4 ? MHS_ROW_GMIN : 8;
     while (2 * G <= avg / 4 && G < MHS_MASK_GMAX) G <<= 1;
     const int rpb = 256 / G;
     const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
     switch (G) {
+    case 4: hipLaunchKernelGGL(k_mask_b<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
     case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
     case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
     case 32: hipLaunchKernelGGL(k_mask_b<32>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
@@ -3083,14 +3098,19 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     const dim3 grid(blocks), blk(256);
 #define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2)
     switch (G) {
+    case 4: MHS_ANALYZE(4); break;
     case 8: MHS_ANALYZE(8); break;
     case 16: MHS_ANALYZE(16); break;
     case 32: MHS_ANALYZE(32); break;
     default: MHS_ANALYZE(64); break;
     }
 #undef MHS_ANALYZE
-    hipLaunchKernelGGL(k_bin_list, dim3((A.M + SCAN_ITEMS - 1) / SCAN_ITEMS), dim3(1024), 0, s, A.M, w.sym_bin,
-                       w.asame, w.grp, w.groups, w.stats->sym_count, w.bin_list);
+    if (scan_per(A.M) == 4)
+        hipLaunchKernelGGL(k_bin_list<4>, dim3((A.M + 4095) / 4096), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
+                           w.groups, w.stats->sym_count, w.bin_list);
+    else
+        hipLaunchKernelGGL(k_bin_list<1>, dim3((A.M + 1023) / 1024), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
+                           w.groups, w.stats->sym_count, w.bin_list);
 }
 
 hipError_t probe_counter(unsigned long long** dev) {
@@ -3217,10 +3237,15 @@ void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, 
 
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
                           Published* pub, int seq) {
-    const int nb = (M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS;  // the state words were zeroed by k_analyze
-    hipLaunchKernelGGL(k_scan, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop, w.rlo,
-                       w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num,
-                       w.blkflop, w.nflop);
+    // the state words were zeroed by k_analyze (SCAN_ITEMS-row blocks: enough for either width)
+    const int per = scan_per(M), nb = (M + 1 + 1024 * per - 1) / (1024 * per);
+#define MHS_SCAN(P)                                                                                                \
+    hipLaunchKernelGGL(k_scan<P>, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop,  \
+                       w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
+                       w.blkflop, w.nflop)
+    if (per == 4) MHS_SCAN(4);
+    else MHS_SCAN(1);
+#undef MHS_SCAN
 }
 
 // Dynamic LDS of a block-kernel launch: the header plus its largest row's tables, in
