@@ -155,10 +155,11 @@ void pool_put(mhs_ctx* ctx, void* p) {
 
 struct Layout {
     size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, asame, grp, bin_list, scan_part, mcache,
-        stats, blkflop, total;
+        stats, blkflop, spill_mask, spill_key, lofs, total;
+    long long spill_cap;
 };
 
-Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list) {
+Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_total = -1) {
     Layout L{};
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -185,6 +186,13 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list) {
     L.blkflop = take(((size_t)analyze_blocks(nnzA, M) + 1) * 8);
     L.scan_part = take(nscan * 8 + (size_t)CURSOR_INTS * 4);  // look-back words, then the row cursors
     L.mcache = take((size_t)M * mc_stride(mc_list) * 8);
+    L.spill_cap = spill_cap(nnzB);
+    if (M_total > M && M_total > 0)  // a row chunk: its share of the region (spill lists belong to rows)
+        L.spill_cap = std::max<long long>(SPILL_PARTS * 1024, L.spill_cap * M / M_total);
+    if (const char* e = getenv("MHS_SPILL_CAP")) L.spill_cap = atoll(e) < 1 ? 1 : atoll(e);  // tests: a full region
+    L.spill_mask = take((size_t)L.spill_cap * 8);
+    L.spill_key = take((size_t)L.spill_cap * 4);
+    L.lofs = take((size_t)M * 4);
     L.total = o;
     return L;
 }
@@ -243,6 +251,11 @@ Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, int Bn, int
     w.cursors = w.scan_part + 2 * ((M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1);
     w.mcache = ctx->use_mcache ? (unsigned long long*)(ctx->ws + L.mcache) : nullptr;
     w.mc_list = mc_list;
+    w.spill.mask = (unsigned long long*)(ctx->ws + L.spill_mask);
+    w.spill.key = (int*)(ctx->ws + L.spill_key);
+    w.spill.lofs = (int*)(ctx->ws + L.lofs);
+    w.spill.top = w.cursors + SPILL_CURSOR_SLOT * 8 * CURSOR_STRIDE;  // zeroed with the cursors
+    w.spill.cap = L.spill_cap;
     w.stats = (Stats*)(ctx->ws + L.stats);
     w.gscratch = ctx->gscratch;
     w.gscratch_bytes = ctx->gscratch_bytes;
@@ -339,7 +352,7 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
         ctx->ws_bytes = 0;
         ctx->stats_zero = false;
         mc_list = ctx->mc_list > 0 ? ctx->mc_list : mc_list_for(Mc);
-        L = plan(Mc, MB, A->nnz, B->nnz, mc_list);
+        L = plan(Mc, MB, A->nnz, B->nnz, mc_list, M);
         int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
         if (rc == MHS_ERR_OOM) {
             (void)hipGetLastError();

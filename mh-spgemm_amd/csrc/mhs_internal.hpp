@@ -37,6 +37,9 @@ constexpr int SCAN_ITEMS = MHS_SCAN_ITEMS;  // rows per block (of 1024 threads) 
 constexpr int CURSOR_SLOTS = 40;
 constexpr int CURSOR_STRIDE = 16;  // ints
 constexpr int CURSOR_INTS = CURSOR_SLOTS * 8 * CURSOR_STRIDE;
+constexpr int SPILL_PARTS = 64;        // spill-list bump counters: cursor slots 32..39
+constexpr int SPILL_CURSOR_SLOT = 32;
+static_assert(SPILL_CURSOR_SLOT * 8 + SPILL_PARTS <= CURSOR_SLOTS * 8, "spill counters fit the cursor area");
 
 // Symbolic bins (by LDS need and tile work).
 // Tiny rows: a team of W lanes per row holding K products per lane (flop <= W*K,
@@ -313,6 +316,20 @@ struct Csr {
     const double* val;
 };
 
+struct SpillLists;  // (mhs_kernels.hip) symbolic's tile lists of rows past the row-cache cap
+struct SpillArea {
+    unsigned long long* mask;
+    int* key;
+    int* lofs;
+    int* top;
+    long long cap;
+};
+// entries of the spill region: one per B nonzero (at least 1 M, at most 64 M = 768 MB)
+inline long long spill_cap(long long nnzB) {
+    const long long c = nnzB < (1LL << 20) ? (1LL << 20) : nnzB;
+    return c > (1LL << 26) ? (1LL << 26) : c;
+}
+
 struct Work {
     // B side
     int* btcol;
@@ -337,6 +354,7 @@ struct Work {
     int* cursors;      // CURSOR_INTS row cursors (after the look-back words)
     unsigned long long* mcache;   // [M][mc_stride] tile masks / tile lists (symbolic -> numeric)
     int mc_list;                  // list cap (see mlisted)
+    SpillArea spill;              // tile lists of rows past mc_list (symbolic -> numeric)
     Stats* stats;
     void* gscratch;    // global-bin scratch
     size_t gscratch_bytes;

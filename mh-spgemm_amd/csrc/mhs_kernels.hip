@@ -357,6 +357,9 @@ struct RowWalk {
     }
 };
 
+#ifndef MHS_SPILL
+#define MHS_SPILL 1  // symbolic keeps the tile lists of rows past the row-cache cap for numeric
+#endif
 #ifndef MHS_WAVE_CHUNKS
 #define MHS_WAVE_CHUNKS 0  // > 0: block teams walk rows of >= this many A entries per thread wave-by-wave
                            // (measured: webbase-like numeric +10%, wb-edu-like symbolic -8%: off)
@@ -403,6 +406,7 @@ struct WaveTeam {
     static constexpr int size = 64;
     __device__ int rank() const { return lane_id(); }
     __device__ void sync() const { wave_sync(); }
+    __device__ int bcast0(int v) const { return __builtin_amdgcn_readfirstlane(v); }  // (lane 0 is active)
     template <class V>
     __device__ V sum(V v) const { return wave_sum(v); }
     template <class LD, class ST>
@@ -428,6 +432,14 @@ struct BlockTeam {
     __device__ void sync() const {
         if constexpr (GLOBALMEM) __threadfence();
         __syncthreads();
+    }
+    __device__ int bcast0(int v) const {  // thread 0's v in every thread
+        __syncthreads();
+        if (threadIdx.x == 0) scratch[0] = v;
+        __syncthreads();
+        const int r = (int)scratch[0];
+        __syncthreads();
+        return r;
     }
     template <class V>
     __device__ V sum(V v) const {
@@ -1680,6 +1692,37 @@ __host__ __device__ inline long long span_bits_bytes(int span) {
     return align16(nw * 8) + align16(nw * 4);
 }
 
+// Spill lists: the (mask, key) tile list of a row with more tiles than its row-cache slot
+// holds (hub rows: hundreds to thousands of tiles), in one bump-allocated region; numeric
+// then skips its tile walk (for span-ranked rows: both).  lofs[row] = the list's offset, or
+// -1 when the region was full; written by symbolic for exactly the rows numeric asks about
+// (not cached, t > mc_list), so it needs no initialisation.
+struct SpillLists : SpillArea {
+    __host__ __device__ SpillLists() : SpillArea{} {}
+    __host__ __device__ SpillLists(const SpillArea& x) : SpillArea(x) {}
+};
+__device__ __forceinline__ bool spill_row(int span, int tflop, int t, int mc_list) {
+    return !mcached(span, tflop) && t > mc_list;
+}
+// Reserve t entries (team-uniform result: offset, or -1 when full) and record it for R rows.
+// The region is cut into SPILL_PARTS partitions with a bump counter each (row % SPILL_PARTS
+// picks one, counters 64 B apart): one counter for every spilling row serialised the
+// symbolic phase on its atomics (wb-edu-like: hundreds of thousands of rows).
+__device__ __forceinline__ int spill_reserve_off(const SpillLists& sp, int row, int t) {
+    const int p = row & (SPILL_PARTS - 1);
+    const long long part = sp.cap / SPILL_PARTS;
+    const int o = atomicAdd(sp.top + p * CURSOR_STRIDE, t);
+    return (long long)o + t <= part ? (int)(p * part + o) : -1;
+}
+template <class Team>
+__device__ __forceinline__ int spill_reserve(const Team& tm, const SpillLists& sp, int row, int R, int t) {
+    int off = -1;
+    if (tm.rank() == 0 && sp.mask) off = spill_reserve_off(sp, row, t);
+    off = tm.bcast0(off);
+    if (tm.rank() < R) sp.lofs[row + tm.rank()] = off;
+    return off;
+}
+
 // ------------------------------------------------------------- symbolic ---
 struct SymArgs {
     int M;
@@ -1702,6 +1745,7 @@ struct SymArgs {
     unsigned long long* mcache;
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
     int* cursors;            // all row cursors (slot NUM_NB + bin: MHS_DYN)
+    SpillLists sp;           // tile lists of rows past the row cache's cap
 };
 
 // Symbolic tile table (counts only, no ranks): masks Mk[H], then -- hashed -- keys Kk[H]:
@@ -1795,6 +1839,37 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
                 }
             }
             k += __popcll(bal);
+        }
+    }
+    // ... rows past the slot: a spill list (one copy for the group: lofs points every row at it)
+    if (MHS_SPILL && a.mcache && spill_row(span, tflop, t, a.mc_list)) {
+        const int off = spill_reserve(tm, a.sp, row, R, t);
+        if (off >= 0) {
+            // every wave compacts its share of the slots (the list is unordered): a wave
+            // team walks all of them, a block's waves take places with an LDS counter
+            // (the stage area is free after the walk)
+            const int lane = lane_id();
+            int* ctr = reinterpret_cast<int*>(stage);
+            if (Team::size > 64 && tm.rank() == 0) *ctr = 0;
+            tm.sync();
+            int k = off;
+            for (int s0 = tm.rank() & ~63; s0 < H; s0 += Team::size) {
+                const int sl = s0 + lane;
+                const unsigned long long m = sl < H ? Mk[sl] : 0ull;
+                const bool occ = m != 0ull;
+                const unsigned long long bal = __ballot(occ);
+                if (Team::size > 64) {
+                    int at = 0;
+                    if (lane == 0 && bal) at = atomicAdd(ctr, __popcll(bal));
+                    k = off + __shfl(at, 0);
+                }
+                if (occ) {
+                    const int pos = k + __popcll(bal & lanemask_lt());
+                    st_cache(&a.sp.mask[pos], m);
+                    st_cache(&a.sp.key[pos], direct ? lo + sl : Kk[sl]);
+                }
+                if (Team::size == 64) k += __popcll(bal);
+            }
         }
     }
     tm.sync();
@@ -1893,6 +1968,7 @@ __device__ void sym_row_wide(const BlockTeam<1024, false>& tm, const SymArgs& a,
     if (tm.rank() < R) {
         a.Cptr[row + tm.rank()] = (int)n;
         a.ctiles[row + tm.rank()] = t;
+        if (a.mcache && spill_row(hi - lo + 1, tflop, t, a.mc_list)) a.sp.lofs[row + tm.rank()] = -1;  // no list
     }
     tm.sync();
 }
@@ -1945,6 +2021,14 @@ __device__ bool sym_row_bitmap(const BlockTeam<1024, false>& tm, const SymArgs& 
                 st_cache(&slot[r], msk[r]);
                 st_cache(&reinterpret_cast<int*>(slot + a.mc_list)[r], kb[r].x);
             }
+    if (MHS_SPILL && a.mcache && spill_row(span, tflop, t, a.mc_list)) {  // in column order
+        const int off = spill_reserve(tm, a.sp, row, R, t);
+        if (off >= 0)
+            for (int r = tm.rank(); r < t; r += T) {
+                st_cache(&a.sp.mask[off + r], msk[r]);
+                st_cache(&a.sp.key[off + r], kb[r].x);
+            }
+    }
     tm.sync();
     return true;
 }
@@ -2277,6 +2361,7 @@ struct NumArgs {
     const unsigned long long* mcache;
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
     int* cursor;             // this launch's 8 row cursors (MHS_DYN)
+    SpillLists sp;           // tile lists of rows past the row cache's cap (symbolic -> numeric)
 };
 
 template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
@@ -2302,6 +2387,9 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     // symbolic kept the masks unless it sorted the row as a tiny one (numeric runs those
     // with tables when the tiny classes are off: N beyond the packed keys' 23 bits)
     const bool sym_tiny = tiny_class_sym(__builtin_amdgcn_readfirstlane(a.rflop[row]), a1 - a0) >= 0;
+    const int lofs = (MHS_SPILL && a.mcache && !sym_tiny && spill_row(span, tflop, t, a.mc_list))
+                         ? __builtin_amdgcn_readfirstlane(a.sp.lofs[row])
+                         : -1;
     // hashed rows rank their tiles by a bitmap over the span (block teams / many tiles,
     // when it fits the accumulator), else by counting (few tiles), else by a sort
     const bool rank_bitmap = MODE == NM_HASH && (Team::size > 64 || t >= 64) &&
@@ -2319,16 +2407,18 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             E[s] = z;
         }
         tm.sync();
-    } else if (a.mcache && mlisted(span, tflop, t, a.mc_list) && !sym_tiny) {
-        // symbolic's compacted list of the t (key, mask) pairs; a hashed row that ranks by
-        // counting also gets its (key, slot | popc) list here, no table compaction later
+    } else if (a.mcache && !sym_tiny && (mlisted(span, tflop, t, a.mc_list) || lofs >= 0)) {
+        // symbolic's compacted list of the t (key, mask) pairs (the row-cache slot, or a spill
+        // list); a hashed row that ranks by counting also gets its (key, slot | popc) list
+        // here, no table compaction later
         clear_tiles(tm, E, H);
         if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
         tm.sync();
-        const unsigned long long* slot = a.mcache + (size_t)row * a.mc_stride;
+        const unsigned long long* slot = lofs >= 0 ? a.sp.mask + lofs : a.mcache + (size_t)row * a.mc_stride;
+        const int* skey = lofs >= 0 ? a.sp.key + lofs : reinterpret_cast<const int*>(slot + a.mc_list);
         for (int r = tm.rank(); r < t; r += Team::size) {
             const unsigned long long m = ld_cache(&slot[r]);
-            const int key = ld_cache(&reinterpret_cast<const int*>(slot + a.mc_list)[r]);
+            const int key = ld_cache(&skey[r]);
             if (MODE != NM_HASH) {
                 E[key - lo].mask = m;
             } else {
@@ -2680,15 +2770,36 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
     int2* kb = (int2*)(region + sb + align16((long long)t * 8));
     double* acc = (double*)(region + sb + 2 * align16((long long)t * 8));
     const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
+    const int lofs = (MHS_SPILL && a.mcache && spill_row(span, tflop, t, a.mc_list))
+                         ? __builtin_amdgcn_readfirstlane(a.sp.lofs[row])
+                         : -1;
     for (int i = tm.rank(); i < nw; i += T) bm[i] = 0ull;
     for (int r = tm.rank(); r < t; r += T) msk[r] = 0ull;
     tm.sync();
-    walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop, SpanBits{bm, lo, a.btcol}, stage);
-    tm.sync();
-    tm.exclusive_scan(
-        nw, [&](int i) { return (int)__popcll(bm[i]); }, [&](int i, int v) { wpre[i] = v; });
-    walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop,
-                  RankedMasks{bm, wpre, msk, kb, lo, a.btcol, a.btmask}, stage);
+    if (lofs >= 0) {
+        // symbolic's spill list (column order): the bits and the ranked masks from t entries
+        // instead of two walks over every product of the row
+        for (int r = tm.rank(); r < t; r += T) {
+            const int d = ld_cache(&a.sp.key[lofs + r]) - lo;
+            atomicOr(&bm[d >> 6], 1ull << (d & 63));
+        }
+        tm.sync();
+        tm.exclusive_scan(
+            nw, [&](int i) { return (int)__popcll(bm[i]); }, [&](int i, int v) { wpre[i] = v; });
+        for (int r = tm.rank(); r < t; r += T) {
+            const int key = ld_cache(&a.sp.key[lofs + r]);
+            const int k = span_rank(bm, wpre, key - lo);
+            msk[k] = ld_cache(&a.sp.mask[lofs + r]);
+            kb[k].x = key;
+        }
+    } else {
+        walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop, SpanBits{bm, lo, a.btcol}, stage);
+        tm.sync();
+        tm.exclusive_scan(
+            nw, [&](int i) { return (int)__popcll(bm[i]); }, [&](int i, int v) { wpre[i] = v; });
+        walk_products(tm, a0, a1, a.Acol, nullptr, a.bmeta, true, tflop,
+                      RankedMasks{bm, wpre, msk, kb, lo, a.btcol, a.btmask}, stage);
+    }
     tm.sync();
     tm.exclusive_scan(
         t, [&](int r) { return (int)__popcll(msk[r]); }, [&](int r, int v) { kb[r].y = v; });
@@ -3198,6 +3309,7 @@ static SymArgs sym_args(const Csr& A, const Work& w, int M, int N, int* Cptr) {
     a.mc_list = w.mc_list;
     a.mc_stride = mc_stride(w.mc_list);
     a.cursors = w.cursors;
+    a.sp = w.spill;
     a.bin = 0;
     return a;
 }
@@ -3308,6 +3420,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     a.gbytes = 0;
     a.grp = w.grp;
     a.cursor = w.cursors;
+    a.sp = w.spill;
 
     // Largest bins first so the long rows start early.
     if (h.num_count[NUM_GLOBAL] > 0) {

@@ -532,3 +532,21 @@ def test_probe_conflict_counter():
     env.pop("MHS_LIB")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert "REFUSED 3" in out.stdout, out.stdout + out.stderr[-2000:]
+
+
+@pytest.mark.parametrize("cap", [None, "300"])
+def test_spill_lists_and_full_region(tool, cap, monkeypatch):
+    # rows with more tiles than the row-cache slot (here a 16-tile slot) hand their tile list
+    # to numeric through the spill region; with a 300-entry region most rows find it full
+    # (lofs = -1) and numeric walks their tiles again -- same C either way
+    if cap:
+        monkeypatch.setenv("MHS_SPILL_CAP", cap)
+    monkeypatch.setenv("MHS_MC_LIST", "16")
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        A = synth.SYNTH["webbase-1M"]() if cap is None else synth.scircuit_like()
+        check(t2, A, A, ref_rule=cap is not None)
+        (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = bin_zoo()
+        check(t2, mhspgemm.CSR(M, K, Ap, Ac, Av), mhspgemm.CSR(K2, N, Bp, Bc, Bv))
+    finally:
+        t2.close()
