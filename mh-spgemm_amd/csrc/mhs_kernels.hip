@@ -209,9 +209,23 @@ __device__ __forceinline__ int hi_lo_span(int lo, int hi) { return hi - lo + 1; 
 #ifndef MHS_NT
 #define MHS_NT 1
 #endif
+#ifndef MHS_NT_PART
+#define MHS_NT_PART 0
+#endif
 template <class T>
 __device__ __forceinline__ void st_stream(T* p, T v) {
 #if MHS_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+// Stores that leave partial cache lines (a tile's set bits, a tiny row's segment ends) stay
+// cached: L2 merges them into whole lines; nontemporal they reach HBM as masked partial
+// writes (measured: WRITE_SIZE 1.32x C's bytes on cant-like).
+template <class T>
+__device__ __forceinline__ void st_part(T* p, T v) {
+#if MHS_NT_PART
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;
@@ -2573,8 +2587,8 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             if ((e.mask >> lane) & 1ull) {
                 const int pos = c0 + e.base + __popcll(e.mask & lanemask_lt());
                 for (int g = 0; g < (GROUPED ? R : 1); ++g) {
-                    st_stream(&a.Ccol[pos + g * n], colbase + (s << TILE_SHIFT) + lane);
-                    st_stream(&a.Cval[pos + g * n], acc[g * stride + (s << TILE_SHIFT) + lane]);
+                    st_part(&a.Ccol[pos + g * n], colbase + (s << TILE_SHIFT) + lane);
+                    st_part(&a.Cval[pos + g * n], acc[g * stride + (s << TILE_SHIFT) + lane]);
                 }
             }
         }
@@ -2590,7 +2604,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                 const int key = MODE != NM_HASH ? lo + s : e.key;
                 if (e.mask && ((e.mask >> lane) & 1ull)) {
                     const int pos = c0 + e.base + __popcll(e.mask & lanemask_lt());
-                    for (int g = 0; g < (GROUPED ? R : 1); ++g) st_stream(&a.Ccol[pos + g * n], (key << TILE_SHIFT) + lane);
+                    for (int g = 0; g < (GROUPED ? R : 1); ++g) st_part(&a.Ccol[pos + g * n], (key << TILE_SHIFT) + lane);
                 }
             }
         } else {
@@ -2719,7 +2733,7 @@ __device__ void num_row_wide(const BlockTeam<T, false>& tm, const NumArgs& a, in
                 unsigned long long m = masks[k];
                 wc += __popcll(m);
                 while (m) {
-                    st_stream(&a.Ccol[c0 + idx++], ((w0 + k) << TILE_SHIFT) + __builtin_ctzll(m));
+                    st_part(&a.Ccol[c0 + idx++], ((w0 + k) << TILE_SHIFT) + __builtin_ctzll(m));
                     m &= m - 1;
                 }
             }
@@ -3077,8 +3091,8 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
                 const unsigned long long hb = __ballot(head[i]) & tmask;
                 if (live && last) {
                     const int pos = c0 + rank0 + __popcll(hb & (below | (1ull << lane))) - 1;
-                    st_stream(&a.Ccol[pos], c[i]);
-                    st_stream(&a.Cval[pos], sum);
+                    st_part(&a.Ccol[pos], c[i]);
+                    st_part(&a.Cval[pos], sum);
                 }
                 carry = __shfl(sum, tb + W - 1);
                 rank0 += __popcll(hb);
