@@ -96,11 +96,16 @@ int mhs_ctx_trim(mhs_ctx *ctx);
  *   MHS_OPT_MEM_BUDGET (default 0 = none): treat a call's workspace, or workspace
  *     plus C, beyond `value` MiB as an out-of-memory condition (exercises the
  *     row-chunked fallback below without filling the device).
+ *   MHS_OPT_TINY_FIRST_ROWS (default 524288; < 0: never): from this many rows of A
+ *     on, rows of at most 128 products are summed during the symbolic phase into
+ *     cached value slots and numeric only copies them into C (one sort instead of
+ *     two; one more device-to-host hand-off per call, so big matrices only).
  * Out of memory: when the workspace, or C beside it, does not fit, mhs_spgemm gives
  * back every cached buffer and retries row-chunked (the workspace sized for half the
  * rows, halved until it fits; C sized by a counting pass and allocated once); it
  * returns MHS_ERR_OOM only when C itself or a one-row workspace does not fit. */
-typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2, MHS_OPT_MEM_BUDGET = 3 } mhs_option;
+typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2, MHS_OPT_MEM_BUDGET = 3,
+                           MHS_OPT_TINY_FIRST_ROWS = 4 } mhs_option;
 int mhs_ctx_set_option(mhs_ctx *ctx, int option, int value);
 /* Calls of this context that ran row-chunked (the out-of-memory fallback). */
 long long mhs_ctx_chunked_calls(const mhs_ctx *ctx);

@@ -48,6 +48,13 @@ struct mhs_ctx {
     bool stats_zero = false; // the workspace's device Stats are zero (left so by the last k_scan)
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     bool tiny_num = true;    // numeric tiny (sort) classes (MHS_NO_TINY_NUM=1: off)
+    // numeric-first tiny rows from this many rows of A on (MHS_OPT_TINY_FIRST_ROWS,
+    // MHS_NFT_MIN_M; < 0: never): one hand-off more per call, so big matrices only
+    long long nft_min_m = 1 << 19;
+    bool nft_slots = true;   // MHS_NFT_NO_SLOTS=1 (tests): count the rows only, as when the slots do not fit
+    int nft_other_pct = 5;   // slots only when at most this share of the rows is past the tiny classes (MHS_NFT_OTHER_PCT)
+    char* slots = nullptr;   // their value slots (cached across calls)
+    size_t slots_bytes = 0;
     size_t mem_budget = 0;   // MHS_OPT_MEM_BUDGET (MiB): a call's workspace + C beyond it count as OOM (tests)
     long long chunked_calls = 0;  // calls that ran row-chunked (mhs_ctx_chunked_calls)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
@@ -155,7 +162,7 @@ void pool_put(mhs_ctx* ctx, void* p) {
 
 struct Layout {
     size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, asame, grp, bin_list, scan_part, mcache,
-        stats, blkflop, spill_mask, spill_key, lofs, total;
+        stats, blkflop, spill_mask, spill_key, lofs, tslot, nft_bin, total;
     long long spill_cap;
 };
 
@@ -193,6 +200,8 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     L.spill_mask = take((size_t)L.spill_cap * 8);
     L.spill_key = take((size_t)L.spill_cap * 4);
     L.lofs = take((size_t)M * 4);
+    L.tslot = take((size_t)M * 8);
+    L.nft_bin = take((size_t)M);
     L.total = o;
     return L;
 }
@@ -256,6 +265,7 @@ Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, int Bn, int
     w.spill.lofs = (int*)(ctx->ws + L.lofs);
     w.spill.top = w.cursors + SPILL_CURSOR_SLOT * 8 * CURSOR_STRIDE;  // zeroed with the cursors
     w.spill.cap = L.spill_cap;
+    w.tslot = (long long*)(ctx->ws + L.tslot);
     w.stats = (Stats*)(ctx->ws + L.stats);
     w.gscratch = ctx->gscratch;
     w.gscratch_bytes = ctx->gscratch_bytes;
@@ -310,8 +320,9 @@ int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h) {
 void free_cached(mhs_ctx* ctx) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->gscratch) (void)hipFree(ctx->gscratch);
-    ctx->ws = ctx->gscratch = nullptr;
-    ctx->ws_bytes = ctx->gscratch_bytes = 0;
+    if (ctx->slots) (void)hipFree(ctx->slots);
+    ctx->ws = ctx->gscratch = ctx->slots = nullptr;
+    ctx->ws_bytes = ctx->gscratch_bytes = ctx->slots_bytes = 0;
     for (auto& b : ctx->pool) (void)hipFree(b.first);
     ctx->pool.clear();
     ctx->stats_zero = false;
@@ -478,6 +489,9 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_MC_LIST")) ctx->mc_list = atoi(e) < MC_LIST_MIN ? MC_LIST_MIN : atoi(e);
     if (getenv("MHS_NO_GROUPS")) ctx->groups = false;
     if (getenv("MHS_NO_TINY_NUM")) ctx->tiny_num = false;
+    if (const char* e = getenv("MHS_NFT_MIN_M")) ctx->nft_min_m = atoll(e);
+    if (getenv("MHS_NFT_NO_SLOTS")) ctx->nft_slots = false;
+    if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     *out = ctx;
     return MHS_OK;
 }
@@ -529,8 +543,9 @@ int mhs_ctx_trim(mhs_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->gscratch) (void)hipFree(ctx->gscratch);
-    ctx->ws = ctx->gscratch = nullptr;
-    ctx->ws_bytes = ctx->gscratch_bytes = 0;
+    if (ctx->slots) (void)hipFree(ctx->slots);
+    ctx->ws = ctx->gscratch = ctx->slots = nullptr;
+    ctx->ws_bytes = ctx->gscratch_bytes = ctx->slots_bytes = 0;
     for (auto& b : ctx->pool) (void)hipFree(b.first);
     ctx->pool.clear();
     return MHS_OK;
@@ -603,12 +618,51 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     launch_mask_b(b, w, s);
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[1], s));
     // ---- symbolic_binning ---------------------------------------------------------
-    launch_analyze(a, w, MB, s, out.ptr);
+    // numeric-first tiny rows (big M): k_analyze also bins the rows that way and counts
+    // them; the host picks the bin lists and sizes the candidates' value slots
+    const bool probe = w.tiny_num && ctx->nft_min_m >= 0 && M >= ctx->nft_min_m && M > 0;
+    unsigned long long other = 0;
+    if (probe) w.nft_bin = (unsigned char*)(ctx->ws + L.nft_bin);
+    const int seq_probe = probe ? ++ctx->seq : 0;
+    launch_analyze(a, w, MB, s, out.ptr, ctx->d_pub, seq_probe);
+    if (probe) {
+        MHS_HIP(hipGetLastError());
+        rc = wait_published(ctx, s, ctx->pub, seq_probe);
+        if (rc) {
+            pool_put(ctx, out.ptr);
+            return rc;
+        }
+        const unsigned long long n = ctx->pub->stats.an_slots;
+        other = ctx->pub->stats.an_other;
+        // slots pay where the tiny rows are (nearly) the whole product: elsewhere numeric's
+        // tiny classes run beside the long rows' kernels anyway (measured: wb-edu-like +10%
+        // with slots, 19% of its rows past the tiny classes; GAP-road- / delaunay-like -12% / -17%)
+        if (n > 0 && ctx->nft_slots && other * 100 <= (unsigned long long)M * ctx->nft_other_pct &&
+            ensure(ctx, &ctx->slots, &ctx->slots_bytes, (size_t)n * 12) == MHS_OK) {
+            w.nft = 1;
+            w.sc_val = (double*)ctx->slots;
+            w.sc_col = (int*)(ctx->slots + (size_t)n * 8);
+        } else {
+            (void)hipGetLastError();
+        }
+        launch_bin_list(a, w, s);
+    }
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[2], s));
     // ---- Calculate_C_nnz ------------------------------------------------------------
-    // persistent grids that read their bins' sizes on the device: no host round trip
-    launch_symbolic_common(a, b, w, M, N, out.ptr, s);
-    launch_symbolic_rare(a, w, M, N, out.ptr, s);
+    // persistent grids that read their bins' sizes on the device: no host round trip.
+    // Numeric-first: rows of the rare bins (long, few) run on an aux stream beside the
+    // common bins -- their tail no longer idles the chip
+    if (w.nft && other > 0 && ctx->num_streams > 1 && ctx->aux[0]) {
+        MHS_HIP(hipEventRecord(ctx->fork_ev, s));
+        MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
+        launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0]);
+        launch_symbolic_common(a, b, w, M, N, out.ptr, s);
+        MHS_HIP(hipEventRecord(ctx->join_ev[0], ctx->aux[0]));
+        MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[0], 0));
+    } else {
+        launch_symbolic_common(a, b, w, M, N, out.ptr, s);
+        launch_symbolic_rare(a, w, M, N, out.ptr, s);
+    }
     MHS_HIP(hipGetLastError());
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
@@ -777,6 +831,9 @@ int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
     case MHS_OPT_MEM_BUDGET:
         if (value < 0) return fail(ctx, MHS_ERR_INVALID, "memory budget must be >= 0 MiB");
         ctx->mem_budget = (size_t)value << 20;
+        return MHS_OK;
+    case MHS_OPT_TINY_FIRST_ROWS:
+        ctx->nft_min_m = value;
         return MHS_OK;
     default:
         return fail(ctx, MHS_ERR_INVALID, "unknown option");

@@ -154,6 +154,9 @@ struct Stats {
     int num_global_need;           // max LDS-equivalent bytes of a global numeric row
     int num_block_need[2];         // max LDS bytes of a row in NUM_B256 / NUM_B1024 (launch sizing)
     int final_done;                // k_scan_final blocks finished (last one publishes)
+    unsigned long long an_slots;   // numeric-first probe: the candidates' slot entries,
+    unsigned long long an_other;   // rows with products past the tiny classes,
+    int an_done;                   // and k_probe_publish blocks finished
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
 // kernel writes it and then `seq`, the host spins on `seq` instead of a stream sync.
@@ -347,6 +350,15 @@ struct Work {
     unsigned char* grp;      // M: row groups (k_bin_list; see RG_MAX)
     int groups;              // form row groups (0: every row alone)
     int tiny_num;            // numeric tiny classes allowed (per row: column span <= TINY_NUM_NMAX + 1)
+    // numeric-first tiny rows (big M): the symbolic tiny launch sorts them once, in the
+    // numeric classes, and sums their values into slots (sc_*); numeric only copies them
+    // into C.  nft_bin (M, the probe): k_analyze also bins every row that way and counts
+    // the candidates; the host then picks the bin lists (nft: numeric-first, with slots).
+    unsigned char* nft_bin;
+    int nft;
+    long long* tslot;        // M: a slot row's first entry
+    int* sc_col;
+    double* sc_val;
     int* bin_list;           // (NUM_NB-1) * M: bin x's rows at (x-1)*M (symbolic bins, then numeric bins)
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count
@@ -361,7 +373,12 @@ struct Work {
 };
 
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);
-void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr);
+// Row analysis, then the symbolic bin lists -- or, with w.nft_bin (the numeric-first
+// probe), the candidate counts published as `seq` (the host then calls launch_bin_list)
+void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr, Published* pub = nullptr,
+                    int seq = 0);
+void launch_bin_list(const Csr& A, const Work& w, hipStream_t s);
+
 int analyze_blocks(long long nnzA, int M);
 
 void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s);

@@ -833,7 +833,8 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
                                                  int* __restrict__ rtflop, int* __restrict__ rlo,
                                                  int* __restrict__ rhi, int* __restrict__ ctiles,
                                                  unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
-                                                 unsigned char* __restrict__ asame, int& err) {
+                                                 unsigned char* __restrict__ asame, int& err,
+                                                 unsigned char* __restrict__ nft_bin, int& nslots, int& nother) {
     const int gl = lane_id() & (G - 1);
     long long flop = 0, tflop = 0;
     int lo = INT_MAX, hi = -1;
@@ -886,6 +887,14 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         const int tc = tiny_class_sym(f, nA);
         const int bin = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
+        if (nft_bin) {
+            // numeric-first candidates: the numeric classes 0..3, whose sort keys hold the
+            // column relative to the row's first tile (23 bits); a wider row counts in a table
+            const int tn = (long long)span * TILE_BITS - 1 <= TINY_NUM_NMAX ? tiny_class(f, nA, TINY_SYM_NC) : -1;
+            nft_bin[row] = (unsigned char)(tn >= 0 ? SYM_TINY + tn : tc >= 0 ? sym_bin_of(f, tf, span) : bin);
+            nslots += tn >= 0 ? tiny_w(tn) * tiny_k(tn) : 0;
+            nother += f > 0 && tn < 0;
+        }
         if (bin == SYM_NONE) {
             Cptr[row] = 0;
             ctiles[row] = 0;
@@ -897,6 +906,11 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
 // G lanes per A row; rows longer than AN_LONG*G entries are deferred to whole-wave
 // walks (as in k_mask_b).
 constexpr int AN_LONG = 16;
+// k_analyze's per-block word: flop (< 2^37: <= 64 rows of < 2^31) in the low 40 bits, then
+// 8 bits of rows past the tiny classes (<= 64 per block) and 16 of numeric-first slot
+// entries (<= 64 rows x 128)
+constexpr int BLK_FLOP_BITS = 40, BLK_SLOT_SHIFT = 48;
+constexpr unsigned long long BLK_FLOP_MASK = (1ull << BLK_FLOP_BITS) - 1;
 template <int G>
 __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __restrict__ Aptr,
                                                  const int* __restrict__ Acol,
@@ -908,30 +922,34 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
                                                  unsigned long long* __restrict__ blkflop,
                                                  unsigned char* __restrict__ asame,
                                                  Stats* __restrict__ stats,
-                                                 unsigned long long* __restrict__ lb_state, int nlb) {
+                                                 unsigned long long* __restrict__ lb_state, int nlb,
+                                                 unsigned char* __restrict__ nft_bin) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nlb; i += gridDim.x * blockDim.x)
         lb_state[i] = 0ull;  // k_scan's look-back words (k_scan runs after every analyze block)
     const bool valid = row < M;
-    int err = 0;
+    int err = 0, nslots = 0, nother = 0;
     bool lng = false;
     if constexpr (G < 64) lng = valid && Aptr[row + 1] - Aptr[row] > AN_LONG * G;
     long long flop = analyze_row<G>(row, valid && !lng, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
-                                    ctiles, sym_bin, Cptr, asame, err);
+                                    ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother);
     flop = gl == 0 ? flop : 0;
     if constexpr (G < 64) {
         for (unsigned long long lb = __ballot(lng && gl == 0); lb; lb &= lb - 1) {
             const int r = __shfl(row, __builtin_ctzll(lb));
             const long long f = analyze_row<64>(r, true, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
-                                                ctiles, sym_bin, Cptr, asame, err);
+                                                ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother);
             flop += lane == 0 ? f : 0;
         }
     }
-    // per-block flop partial (plain store; summed by the scan's last block)
+    // per-block flop partial (plain store; summed by k_scan), with the block's other rows and
+    // numeric-first slot entries above bit BLK_FLOP_BITS (summed by k_probe_publish)
     __shared__ unsigned long long wsum[4];
     unsigned long long mine = (unsigned long long)flop;
+    if (nft_bin && gl == 0)
+        mine += ((unsigned long long)nother << BLK_FLOP_BITS) + ((unsigned long long)nslots << BLK_SLOT_SHIFT);
     mine = wave_sum(mine);
     if (lane == 0) wsum[threadIdx.x >> 6] = mine;
     __syncthreads();
@@ -2121,35 +2139,59 @@ __device__ void append_block_rows(const unsigned char* binof, long long M, int* 
 // is too fine-grained for per-block cursor atomics).  Row i's group: the maximal run
 // of same-pattern rows containing it, broken every RG_BREAK rows, cut into groups of
 // RG_MAX from the run start.  Only group heads enter the symbolic lists (a group's
-// rows share one C pattern).
+// rows share one C pattern).  Numeric-first tiny rows stay alone (their values come
+// out of the symbolic pass).
+// Numeric-first probe: sums k_analyze's per-block slot entries / other rows and hands them
+// to the host (the last block publishes), which picks the bin lists.
+__global__ __launch_bounds__(1024) void k_probe_publish(const unsigned long long* __restrict__ blk, int n,
+                                                        Stats* __restrict__ stats, Published* pub, int seq) {
+    const int per = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+    unsigned long long slots = 0, other = 0;
+    for (int i = i0 + threadIdx.x; i < i1; i += 1024) {
+        const unsigned long long x = blk[i];
+        other += (x >> BLK_FLOP_BITS) & 0xFF;
+        slots += x >> BLK_SLOT_SHIFT;
+    }
+    slots = wave_sum(slots);
+    other = wave_sum(other);
+    if (lane_id() == 0 && slots) atomicAdd(&stats->an_slots, slots);
+    if (lane_id() == 0 && other) atomicAdd(&stats->an_other, other);
+    if (last_block_done(&stats->an_done)) publish_stats(stats, pub, seq);
+}
+
 template <int PER>
 __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* __restrict__ bin_id,
                                                    const unsigned char* __restrict__ asame,
                                                    unsigned char* __restrict__ grp, int groups,
-                                                   int* __restrict__ cnt, int* __restrict__ list) {
+                                                   int* __restrict__ list, const unsigned char* __restrict__ nft_bin,
+                                                   Stats* __restrict__ stats) {
     __shared__ unsigned char binof[1024 * PER];
     for (int j = threadIdx.x; j < 1024 * PER; j += 1024) {
         const long long i = (long long)blockIdx.x * (1024 * PER) + j;
         unsigned char b = 0;
         if (i < M) {
             int g = 1;
-            if (groups && asame[i]) {
+            // a run of same-pattern rows is tiny throughout or not at all
+            const int bi = nft_bin ? nft_bin[i] : bin_id[i];
+            const bool solo = nft_bin && bi >= SYM_TINY && bi < SYM_TINY + TINY_SYM_NC;
+            if (groups && !solo && asame[i]) {
                 long long rs = i;
                 const long long lim = i - i % RG_BREAK;
                 while (rs > lim && asame[rs]) --rs;
                 const int o = (int)((i - rs) % RG_MAX);
                 if (o) g = GRP_CONT | o;
             }
-            if (groups && g == 1) {  // a head: count the rows that follow it in its group
+            if (groups && !solo && g == 1) {  // a head: count the rows that follow it in its group
                 while (g < RG_MAX && i + g < M && (i + g) % RG_BREAK != 0 && asame[i + g]) ++g;
             }
             grp[i] = (unsigned char)g;
-            b = (g & GRP_CONT) ? 0 : bin_id[i];
+            b = (g & GRP_CONT) ? 0 : bi;
         }
         binof[j] = b;
     }
     __syncthreads();
-    append_block_rows<SYM_NB, PER>(binof, M, cnt, list, (int)blockIdx.x);
+    append_block_rows<SYM_NB, PER>(binof, M, stats->sym_count, list, (int)blockIdx.x);
 }
 
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
@@ -2202,7 +2244,8 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                const int* __restrict__ Aptr,
                                                int* __restrict__ list, Stats* __restrict__ stats,
                                                int dense_span_max, Published* pub, int seq, int tiny_ok,
-                                               const unsigned long long* __restrict__ blkflop, int nflop) {
+                                               const unsigned long long* __restrict__ blkflop, int nflop, int nft,
+                                               long long* __restrict__ tslot) {
     constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
     static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
@@ -2244,7 +2287,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         const int per = (nflop + (int)gridDim.x - 1) / (int)gridDim.x;
         const int i1 = min(nflop, (bid + 1) * per);
         unsigned long long f = 0;
-        for (int i = bid * per + threadIdx.x; i < i1; i += 1024) f += blkflop[i];
+        for (int i = bid * per + threadIdx.x; i < i1; i += 1024) f += blkflop[i] & BLK_FLOP_MASK;
         f = wave_sum(f);
         if (lane == 0 && f) atomicAdd(&stats->flop, f);
     }
@@ -2266,8 +2309,14 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
             const int nA = Aptr[i + 1] - Aptr[i];
             // tiny sort keys hold the column relative to the row's first tile in 23 bits
             const bool tok = tiny_ok && (long long)span * TILE_BITS - 1 <= TINY_NUM_NMAX;
-            const int gb = num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max, nA, tok);
-            if (gb != NUM_NONE)
+            // numeric-first rows (k_analyze's rule) have their values: one copy list
+            const int fc = nft && tok ? tiny_class(rflop[i], nA, TINY_SYM_NC) : -1;
+            const int gb =
+                fc >= 0 ? -1 : num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max, nA, tok);
+            if (nft && fc < 0) tslot[i] = -1;  // (slot rows: written by the symbolic pass)
+            if (gb < 0)
+                nbin = NUM_TINY + fc;
+            else if (gb != NUM_NONE)
                 nbin = (g & GRP_CONT) ? NUM_NONE : gb;
             else
                 nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max, nA,
@@ -2955,7 +3004,8 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
 // several rows per wave -- where a wave per row would idle most lanes through ten
 // dependent loads.
 struct TinyArgs {
-    int M, count, bin;  // count: numeric only (symbolic reads its bin's size on the device)
+    int M, count, bin;  // count < 0: the bin's size on the device (the symbolic launch)
+    int nft;            // symbolic launch: numeric-first slot rows (the numeric classes; see k_analyze)
     const int* Aptr;
     const int* Acol;
     const double* Aval;
@@ -2970,6 +3020,15 @@ struct TinyArgs {
     int* ctiles;
     int* Ccol;
     double* Cval;
+    // numeric-first: the symbolic launch sums the rows into value slots (class c's from
+    // sbase on: W*K entries per row of its list; a wave's rows packed at the start of
+    // their slots' span), the row's nnz goes to Cptr[row] and its slot to tslot[row];
+    // k_tiny_copy moves them into C
+    int* sc_col;
+    double* sc_val;
+    long long* tslot;
+    long long sbase;
+    int blk0[TINY_SYM_NC + 1];  // slots: class c takes blocks [blk0[c], blk0[c+1]) (sized on the host)
 };
 
 template <int W, int K, bool NUMERIC>
@@ -2980,7 +3039,8 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
     const int tb = lane & ~(W - 1);  // the team's first lane
     const unsigned long long tmask = W == 64 ? ~0ull : (((1ull << (W & 63)) - 1) << tb);
     const unsigned long long below = tmask & lanemask_lt();
-    const int count = NUMERIC ? a.count : a.stats->sym_count[a.bin];
+    const int count = a.count >= 0 ? a.count : a.stats->sym_count[a.bin];
+    const bool slots = NUMERIC && a.sc_col != nullptr;  // numeric-first: into value slots
     const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W), bid, nb);
     extern __shared__ __attribute__((aligned(16))) char tiny_smem[];
     double* vstage = (double*)tiny_smem + (size_t)(threadIdx.x / W) * (W * K);  // numeric: W*K doubles per team
@@ -2989,7 +3049,7 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
         const bool live = it < rw.end;
         const int row = live ? a.list[it] : 0;
         const int a0 = live ? a.Aptr[row] : 0, nA = live ? a.Aptr[row + 1] - a0 : 0;
-        const int c0 = (NUMERIC && live) ? a.Cptr[row] : 0;  // issued early: off the tail's chain
+        long long c0 = (NUMERIC && live && !slots) ? a.Cptr[row] : 0;  // issued early: off the tail's chain
         const int cb = (NUMERIC && live) ? (a.rlo[row] << TILE_SHIFT) : 0;  // key origin (23-bit offsets)
         int st = 0, len = 0;
         double av = 0.0;
@@ -3068,6 +3128,11 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
             nnz += __popcll(__ballot(head[i]) & tmask);
             prev_last = __shfl(c[i], tb + W - 1);
         }
+        if (slots) {  // the wave's rows own the slots of list entries [it0, it0 + 64/W): packed
+            const int x = (tl == 0 && live) ? nnz : 0;
+            const int inc = wave_incl_scan(x);
+            c0 = a.sbase + (long long)__shfl(it, 0) * (W * K) + __shfl(inc - x, tb);
+        }
         if constexpr (!NUMERIC) {
             const int R = live ? (int)a.grp[row] : 0;  // a group head: its rows share the count
             if (tl < R) {
@@ -3090,12 +3155,16 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
                 const bool last = c[i] != INT_MAX && next != c[i];
                 const unsigned long long hb = __ballot(head[i]) & tmask;
                 if (live && last) {
-                    const int pos = c0 + rank0 + __popcll(hb & (below | (1ull << lane))) - 1;
-                    st_part(&a.Ccol[pos], c[i]);
-                    st_part(&a.Cval[pos], sum);
+                    const long long pos = c0 + rank0 + __popcll(hb & (below | (1ull << lane))) - 1;
+                    st_part(&(slots ? a.sc_col : a.Ccol)[pos], c[i]);
+                    st_part(&(slots ? a.sc_val : a.Cval)[pos], sum);
                 }
                 carry = __shfl(sum, tb + W - 1);
                 rank0 += __popcll(hb);
+            }
+            if (slots && live && tl == 0) {
+                a.Cptr[row] = rank0;
+                a.tslot[row] = c0;
             }
         }
     }
@@ -3133,19 +3202,121 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(8) void k_tiny_num_small(TinyArgs
 // [TINY_SYM_GRID*c, TINY_SYM_GRID*(c+1)) walk class c's list.
 constexpr int TINY_SYM_GRID = 1024;
 __device__ __forceinline__ void tiny_sym_rows(TinyArgs a, int blk) {
-    const int c = blk / TINY_SYM_GRID, bid = blk % TINY_SYM_GRID;
+    int c = blk / TINY_SYM_GRID, bid = blk % TINY_SYM_GRID, nb = TINY_SYM_GRID;
+    if (a.nft) {  // numeric-first slots: the grid follows the bins' sizes, as numeric's does
+        // (constant indices only: a dynamically indexed kernel argument goes to scratch)
+        static_assert(TINY_SYM_NC == 4, "class ranges below");
+        const int b1 = a.blk0[1], b2 = a.blk0[2], b3 = a.blk0[3], b4 = a.blk0[4];
+        c = (blk >= b1) + (blk >= b2) + (blk >= b3);
+        const int lo = c == 0 ? 0 : c == 1 ? b1 : c == 2 ? b2 : b3;
+        const int hi = c == 0 ? b1 : c == 1 ? b2 : c == 2 ? b3 : b4;
+        bid = blk - lo;
+        nb = hi - lo;
+    }
     static_assert(TINY_NC == 6 && TINY_SYM_NC == 4 && tiny_ws(3) <= 32 && tiny_w(3) <= 32 && tiny_w(4) == 64 &&
                       tiny_w(5) == 64,
                   "k_tiny_sym / launch_tiny_num instantiate the classes of tiny_class()");
     a.bin = SYM_TINY + c;
     a.list += (long long)c * a.M;
+    if (!a.nft) {
+        switch (c) {
+        case 0: tiny_rows<tiny_ws(0), tiny_ks(0), false>(a, bid, TINY_SYM_GRID); break;
+        case 1: tiny_rows<tiny_ws(1), tiny_ks(1), false>(a, bid, TINY_SYM_GRID); break;
+        case 2: tiny_rows<tiny_ws(2), tiny_ks(2), false>(a, bid, TINY_SYM_GRID); break;
+        default: tiny_rows<tiny_ws(3), tiny_ks(3), false>(a, bid, TINY_SYM_GRID); break;
+        }
+        return;
+    }
+    // numeric-first: the numeric classes' shapes; class c's slots follow classes < c
+    for (int k = 0; k < c; ++k) a.sbase += (long long)a.stats->sym_count[SYM_TINY + k] * (tiny_w(k) * tiny_k(k));
     switch (c) {
-    case 0: tiny_rows<tiny_ws(0), tiny_ks(0), false>(a, bid, TINY_SYM_GRID); break;
-    case 1: tiny_rows<tiny_ws(1), tiny_ks(1), false>(a, bid, TINY_SYM_GRID); break;
-    case 2: tiny_rows<tiny_ws(2), tiny_ks(2), false>(a, bid, TINY_SYM_GRID); break;
-    default: tiny_rows<tiny_ws(3), tiny_ks(3), false>(a, bid, TINY_SYM_GRID); break;
+    case 0: tiny_rows<tiny_w(0), tiny_k(0), true>(a, bid, nb); break;
+    case 1: tiny_rows<tiny_w(1), tiny_k(1), true>(a, bid, nb); break;
+    case 2: tiny_rows<tiny_w(2), tiny_k(2), true>(a, bid, nb); break;
+    default: tiny_rows<tiny_w(3), tiny_k(3), true>(a, bid, nb); break;
     }
 }
+
+// Numeric-first rows: C entries from their value slots, L lanes per row (two entries
+// per lane in flight), class c's list over blocks [f.blk0[k], f.blk0[k+1]).
+#ifndef MHS_COPY_ROWS
+#define MHS_COPY_ROWS 1
+#endif
+struct CopyArgs {
+    const int* list;  // numeric bin lists (class c's at (NUM_TINY + c - 1) * M)
+    long long M;
+    const int* Cptr;
+    const long long* tslot;
+    const int* sc_col;
+    const double* sc_val;
+    int* Ccol;
+    double* Cval;
+};
+template <int L>
+__device__ __forceinline__ void copy_rows(const CopyArgs& a, const int* list, int count, int bid, int nb) {
+    const int tl = threadIdx.x & (L - 1);
+    for (int it = bid * (256 / L) + (int)(threadIdx.x / L); it < count; it += nb * (256 / L)) {
+        const int row = list[it];
+        const int c0 = a.Cptr[row], n = a.Cptr[row + 1] - c0;
+        const long long src = a.tslot[row];
+        for (int k = tl; k < n; k += 2 * L) {
+            const bool two = k + L < n;
+            const int x0 = a.sc_col[src + k];
+            const double v0 = a.sc_val[src + k];
+            const int x1 = two ? a.sc_col[src + k + L] : 0;
+            const double v1 = two ? a.sc_val[src + k + L] : 0.0;
+            a.Ccol[c0 + k] = x0;
+            a.Cval[c0 + k] = v0;
+            if (two) {
+                a.Ccol[c0 + k + L] = x1;
+                a.Cval[c0 + k + L] = v1;
+            }
+        }
+    }
+}
+__global__ __launch_bounds__(256) void k_tiny_copy(CopyArgs a, TinyFused f) {
+    int k = 0;
+    while (k + 1 < f.nclass && (int)blockIdx.x >= f.blk0[k + 1]) ++k;
+    const int bid = (int)blockIdx.x - f.blk0[k], nb = f.blk0[k + 1] - f.blk0[k];
+    const int c = f.c[k], count = f.count[k];
+    const int* list = a.list + (long long)(NUM_TINY + c - 1) * a.M;
+    switch (c) {  // lanes per row ~ a quarter of the class's products
+    case 0: copy_rows<4>(a, list, count, bid, nb); break;
+    case 1: copy_rows<8>(a, list, count, bid, nb); break;
+    case 2: copy_rows<16>(a, list, count, bid, nb); break;
+    default: copy_rows<32>(a, list, count, bid, nb); break;
+    }
+}
+static int copy_lanes(int c) { return c == 0 ? 4 : c == 1 ? 8 : c == 2 ? 16 : 32; }
+
+// The same in row order (MHS_COPY_ROWS): L lanes per row over every row of A, slot rows
+// only (tslot >= 0; k_scan marks the others): a wave's stores cover consecutive C rows
+// and its loads consecutive slots, with no list in the chain.
+template <int L>
+__global__ __launch_bounds__(256) void k_tiny_copy_rows(CopyArgs a) {
+    const int tl = threadIdx.x & (L - 1);
+    for (long long row = ((long long)blockIdx.x * 256 + threadIdx.x) / L; row < a.M;
+         row += (long long)gridDim.x * (256 / L)) {
+        const long long src = a.tslot[row];
+        if (src < 0) continue;
+        const int c0 = a.Cptr[row], n = a.Cptr[row + 1] - c0;
+        for (int k = tl; k < n; k += 2 * L) {
+            const bool two = k + L < n;
+            const int x0 = a.sc_col[src + k];
+            const double v0 = a.sc_val[src + k];
+            const int x1 = two ? a.sc_col[src + k + L] : 0;
+            const double v1 = two ? a.sc_val[src + k + L] : 0.0;
+            a.Ccol[c0 + k] = x0;
+            a.Cval[c0 + k] = v0;
+            if (two) {
+                a.Ccol[c0 + k + L] = x1;
+                a.Cval[c0 + k + L] = v1;
+            }
+        }
+    }
+}
+
+
 
 // The common symbolic bins in one launch (their sizes are on the device; an empty role
 // costs its blocks one load): blocks [0, wave_blocks) run the small-table wave bin,
@@ -3216,12 +3387,12 @@ int analyze_blocks(long long nnzA, int M) {
     return blocks;
 }
 
-void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr) {
+void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr, Published* pub, int seq) {
     if (A.M <= 0) return;
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2)
+#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin)
     switch (G) {
     case 4: MHS_ANALYZE(4); break;
     case 8: MHS_ANALYZE(8); break;
@@ -3230,12 +3401,22 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     default: MHS_ANALYZE(64); break;
     }
 #undef MHS_ANALYZE
+    if (w.nft_bin) {  // numeric-first probe: the counts go to the host, which picks the bin lists
+        hipLaunchKernelGGL(k_probe_publish, dim3(64), dim3(1024), 0, s, (const unsigned long long*)w.blkflop, blocks,
+                           w.stats, pub, seq);
+        return;
+    }
+    launch_bin_list(A, w, s);
+}
+
+void launch_bin_list(const Csr& A, const Work& w, hipStream_t s) {
+    const unsigned char* nb = w.nft ? w.nft_bin : nullptr;
     if (scan_per(A.M) == 4)
         hipLaunchKernelGGL(k_bin_list<4>, dim3((A.M + 4095) / 4096), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
-                           w.groups, w.stats->sym_count, w.bin_list);
+                           w.groups, w.bin_list, nb, w.stats);
     else
         hipLaunchKernelGGL(k_bin_list<1>, dim3((A.M + 1023) / 1024), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
-                           w.groups, w.stats->sym_count, w.bin_list);
+                           w.groups, w.bin_list, nb, w.stats);
 }
 
 hipError_t probe_counter(unsigned long long** dev) {
@@ -3347,7 +3528,25 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
     t.Cptr = Cptr;
     t.ctiles = w.ctiles;
     t.list = w.bin_list + (long long)(SYM_TINY - 1) * M;
-    hipLaunchKernelGGL(k_sym_common<SYM_WAVE_BYTES>, dim3(wave_blocks + TINY_SYM_GRID * TINY_SYM_NC), dim3(256),
+    t.count = -1;
+    t.nft = w.nft;
+    if (w.nft) {
+        t.Aval = A.val;
+        t.Bval = B.val;
+        t.rlo = w.rlo;
+        t.sc_col = w.sc_col;
+        t.sc_val = w.sc_val;
+        t.tslot = w.tslot;
+    }
+    int tiny_blocks = TINY_SYM_GRID * TINY_SYM_NC;
+    if (t.nft) {  // (the classes' sizes are on the device: grids for M rows each, as numeric's)
+        for (int c = 0; c < TINY_SYM_NC; ++c) {
+            const int per = 256 / tiny_w(c);
+            t.blk0[c + 1] = t.blk0[c] + round8((M + per - 1) / per, 4096);
+        }
+        tiny_blocks = t.blk0[TINY_SYM_NC];
+    }
+    hipLaunchKernelGGL(k_sym_common<SYM_WAVE_BYTES>, dim3(wave_blocks + tiny_blocks), dim3(256),
                        WPB * SYM_WAVE_BYTES, s, a, t, wave_blocks);
 }
 
@@ -3368,7 +3567,7 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
 #define MHS_SCAN(P)                                                                                                \
     hipLaunchKernelGGL(k_scan<P>, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop,  \
                        w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
-                       w.blkflop, w.nflop)
+                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot)
     if (per == 4) MHS_SCAN(4);
     else MHS_SCAN(1);
 #undef MHS_SCAN
@@ -3436,6 +3635,43 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     a.cursor = w.cursors;
     a.sp = w.spill;
 
+    // Numeric-first rows: their copy first (short and HBM-bound: it runs beside the long rows'
+    // launches instead of behind one of them).
+    const bool copy = w.sc_col != nullptr;  // numeric-first: tiny classes 0..3 hold slot rows
+    if (copy) {
+        TinyFused f{};
+        int ncopy = 0, cmed = 0;
+        for (int c = 3; c >= 0; --c) {
+            const int count = h.num_count[NUM_TINY + c];
+            if (count <= 0) continue;
+            ncopy += count;
+            const int per = 256 / copy_lanes(c);
+            f.c[f.nclass] = c;
+            f.count[f.nclass] = count;
+            f.blk0[f.nclass + 1] = f.blk0[f.nclass] + round8((count + per - 1) / per, 4096);
+            ++f.nclass;
+        }
+        for (int c = 0, acc = 0; c < 4; ++c) {  // the class of the median slot row
+            acc += h.num_count[NUM_TINY + c];
+            if (2 * acc >= ncopy) {
+                cmed = c;
+                break;
+            }
+        }
+        if (f.nclass > 0) {
+            const CopyArgs ca{w.bin_list, A.M, Cptr, w.tslot, w.sc_col, w.sc_val, Ccol, Cval};
+            s = next_stream();
+            if (MHS_COPY_ROWS) {  // lanes per row by the median row's class
+                const int L = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
+                const dim3 grid(round8((A.M + 256 / L - 1) / (256 / L), 16384));
+                if (L == 4) hipLaunchKernelGGL(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
+                else if (L == 8) hipLaunchKernelGGL(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
+                else hipLaunchKernelGGL(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
+            } else {
+                hipLaunchKernelGGL(k_tiny_copy, dim3(f.blk0[f.nclass]), dim3(256), 0, s, ca, f);
+            }
+        }
+    }
     // Largest bins first so the long rows start early.
     if (h.num_count[NUM_GLOBAL] > 0) {
         const int count = a.count = h.num_count[NUM_GLOBAL];
@@ -3512,7 +3748,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         static_assert(tiny_w(3) <= 32 && tiny_k(0) <= TINY_FUSED_KMAX && tiny_k(1) <= TINY_FUSED_KMAX &&
                           tiny_k(2) <= TINY_FUSED_KMAX && tiny_k(3) <= TINY_FUSED_KMAX && tiny_w(4) == 64,
                       "classes 0..3 fuse (W <= 32, K <= TINY_FUSED_KMAX)");
-        for (int c = 3; c >= 0; --c) {
+        for (int c = 3; c >= 0 && !copy; --c) {  // (numeric-first: copied above)
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;
             const int per = 256 / tiny_w(c);

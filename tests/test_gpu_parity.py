@@ -550,3 +550,40 @@ def test_spill_lists_and_full_region(tool, cap, monkeypatch):
         check(t2, mhspgemm.CSR(M, K, Ap, Ac, Av), mhspgemm.CSR(K2, N, Bp, Bc, Bv))
     finally:
         t2.close()
+
+
+@pytest.mark.parametrize("slots", [True, False])
+def test_numeric_first_tiny_rows(tool, slots, monkeypatch):
+    # numeric-first tiny rows (probed from 512 K rows; here for every size): symbolic sorts
+    # them in the numeric classes and sums them into value slots, numeric copies the slots
+    # into C.  Without slots (no room, or too many other rows) the probe falls back to the
+    # usual bin lists.  Rows spanning past the packed-key range and row groups stay on
+    # their usual paths.
+    if not slots:
+        monkeypatch.setenv("MHS_NFT_NO_SLOTS", "1")
+    monkeypatch.setenv("MHS_NFT_OTHER_PCT", "100")  # slots whatever the share of other rows
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        t2.set_option(mhspgemm._lib.MHS_OPT_TINY_FIRST_ROWS, 0)
+        for seed in (7, 8):
+            (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = tiny_zoo(seed)
+            t = check(t2, mhspgemm.CSR(M, K, Ap, Ac, Av), mhspgemm.CSR(K2, N, Bp, Bc, Bv))
+            assert all(t.sym_bins[i] > 0 for i in range(5, 9)), t.sym_bins
+            # numeric's class lists: copied from the slots, or sorted again without them
+            assert all(t.num_bins[i] > 0 for i in range(8, 12)), t.num_bins
+        (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = group_zoo(3)
+        check(t2, mhspgemm.CSR(M, K, Ap, Ac, Av), mhspgemm.CSR(K2, N, Bp, Bc, Bv))
+        # tiny rows past the 2^23-column key range: tables in both phases
+        K, N = 400, 9_000_000
+        rng = np.random.default_rng(5)
+        Bp = np.arange(0, 2 * K + 1, 2, dtype=np.int32)
+        Bc = np.stack([np.arange(K) * 3, 8_900_000 + np.arange(K)], 1).reshape(-1).astype(np.int32)
+        p, c, v = random_csr(2000, K, 3, seed=6)
+        t = check(t2, mhspgemm.CSR(2000, K, p, c, v), mhspgemm.CSR(K, N, Bp, Bc, rng.uniform(0.5, 1.5, 2 * K)))
+        assert sum(t.num_bins[8:14]) == 0, t.num_bins  # (no candidates: the probe keeps the usual lists)
+        for name in ("scircuit", "webbase-1M", "cant"):
+            A = synth.SYNTH[name]()
+            check(t2, A, A)
+            A.d_release_csr()
+    finally:
+        t2.close()
