@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 5
+#define MHS_ABI_VERSION 6
 
 typedef enum mhs_status {
     MHS_OK = 0,
