@@ -51,6 +51,7 @@ struct mhs_ctx {
     // numeric-first tiny rows from this many rows of A on (MHS_OPT_TINY_FIRST_ROWS,
     // MHS_NFT_MIN_M; < 0: never): one hand-off more per call, so big matrices only
     long long nft_min_m = 1 << 19;
+    bool sym_fork = false;   // MHS_SYM_FORK=1: rare symbolic bins on an aux stream for every call
     bool nft_slots = true;   // MHS_NFT_NO_SLOTS=1 (tests): count the rows only, as when the slots do not fit
     int nft_other_pct = 5;   // slots only when at most this share of the rows is past the tiny classes (MHS_NFT_OTHER_PCT)
     char* slots = nullptr;   // their value slots (cached across calls)
@@ -491,6 +492,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (getenv("MHS_NO_TINY_NUM")) ctx->tiny_num = false;
     if (const char* e = getenv("MHS_NFT_MIN_M")) ctx->nft_min_m = atoll(e);
     if (getenv("MHS_NFT_NO_SLOTS")) ctx->nft_slots = false;
+    if (const char* e = getenv("MHS_SYM_FORK")) ctx->sym_fork = atoi(e) != 0;
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     *out = ctx;
     return MHS_OK;
@@ -652,7 +654,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // persistent grids that read their bins' sizes on the device: no host round trip.
     // Numeric-first: rows of the rare bins (long, few) run on an aux stream beside the
     // common bins -- their tail no longer idles the chip
-    if (w.nft && other > 0 && ctx->num_streams > 1 && ctx->aux[0]) {
+    if (((w.nft && other > 0) || ctx->sym_fork) && ctx->num_streams > 1 && ctx->aux[0]) {
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
         launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0]);

@@ -126,7 +126,10 @@ constexpr int NUM_WS_BYTES = MHS_NUM_WS_BYTES;   // 4 waves x 5 KiB = 20 KiB/blo
 constexpr int NUM_WS_WORK = 8192;       // products a single wave takes on
 constexpr int NUM_W16_BYTES = 16384;
 constexpr int NUM_W16_WORK = 32768;
-constexpr int NUM_WSG_BYTES = 10240;  // grouped rows: 4 waves x 10 KiB = 40 KiB/block (4 per CU)
+#ifndef MHS_NUM_WSG_BYTES
+#define MHS_NUM_WSG_BYTES 10240
+#endif
+constexpr int NUM_WSG_BYTES = MHS_NUM_WSG_BYTES;  // grouped rows: 4 waves x 10 KiB = 40 KiB/block (4 per CU)
 constexpr int NUM_B256_BYTES = 65536;
 constexpr int NUM_B256_WORK = 1 << 22;
 constexpr int LDS_MAX = 163840;         // gfx950: 160 KiB per workgroup (probed on the box)

@@ -2194,6 +2194,9 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
     append_block_rows<SYM_NB, PER>(binof, M, stats->sym_count, list, (int)blockIdx.x);
 }
 
+#ifndef MHS_W16_BLOCK
+#define MHS_W16_BLOCK 0  // 1: rows of the 16 KiB wave bins go to the 256-thread block bin
+#endif
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
                                           int dense_span_max, int nA, bool tiny_ok) {
     if (n == 0) return NUM_NONE;
@@ -2205,7 +2208,7 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
     if (tc >= 0) return NUM_TINY + tc;  // a bigger table than the small wave bin's: sort in registers
     if (num_wide(span, t, n, dense_span_max) || num_ranked(span, t, n, dense_span_max))
         return NUM_B1024;  // rank by span bitmap, else windowed masks with global accumulation
-    if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return hash ? NUM_W16H : NUM_W16;
+    if (!MHS_W16_BLOCK && need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return hash ? NUM_W16H : NUM_W16;
     if (need <= NUM_B256_BYTES - BLOCK_HDR && flop <= NUM_B256_WORK) return NUM_B256;
     if (need <= B1024_BYTES) return NUM_B1024;
     atomicMax(gneed, (int)(need > INT_MAX ? INT_MAX : need));
@@ -2427,6 +2430,36 @@ struct NumArgs {
     SpillLists sp;           // tile lists of rows past the row cache's cap (symbolic -> numeric)
 };
 
+#ifndef MHS_RANK_SORT
+#define MHS_RANK_SORT 0  // register-sort ranking: measured cage15-like +3 %, offshore +2 % (kept off)
+#endif
+constexpr int RANK_SORT_MIN = 32;  // tiles below which counting is as cheap
+// Tile bases of a hashed wave row from its compacted (key, slot << 8 | popc) list L of t
+// tiles (t <= 64 K, keys within 2^23 of lo, slots < 512): E[slot].base = the popcounts of
+// the smaller keys.
+template <int K>
+__device__ __forceinline__ void rank_sorted(TileEntry* E, const int2* L, int t, int lo) {
+    const int lane = lane_id();
+    unsigned k[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const int e = i * 64 + lane;
+        const int2 v = e < t ? L[e] : make_int2(0, 0);
+        k[i] = e < t ? ((unsigned)(v.x - lo) << 9) | (unsigned)(v.y >> 8) : 0xFFFFFFFFu;
+    }
+    reg_bitonic<64, K>(k, lane);
+    int carry = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const bool real = k[i] != 0xFFFFFFFFu;
+        const int slot = (int)(k[i] & 511u);
+        const int p = real ? (int)__popcll(E[slot].mask) : 0;
+        const int inc = wave_incl_scan(p);
+        if (real) E[slot].base = carry + inc - p;
+        carry += __shfl(inc, 63);
+    }
+}
+
 template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
 __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, int span, int t,
                              int c0, int n, int a0, int a1, char* region, int* counter,
@@ -2567,6 +2600,15 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                     make_int2((int)q.w, (s << 8) | __popcll(((unsigned long long)q.y << 32) | q.x));
         }
         tm.sync();
+        if (Team::size == 64 && MHS_RANK_SORT && t > RANK_SORT_MIN && t <= 256 && span <= (1 << 23) && H <= 512) {
+            // wave teams, more than a few dozen tiles: sort (key offset << 9 | slot) in
+            // registers (bitonic over DPP, K = 1 / 2 / 4 keys per lane), then the bases are an
+            // exclusive scan of the popcounts in sorted order -- O(t log^2 t / 64) per lane
+            // instead of the count's t^2 / 64
+            if (t <= 64) rank_sorted<1>(E, L, t, lo);
+            else if (t <= 128) rank_sorted<2>(E, L, t, lo);
+            else rank_sorted<4>(E, L, t, lo);
+        } else
         for (int i = tm.rank(); i < t; i += Team::size) {
             const int2 me = L[i];
             int base = 0, j = MHS_NUM_DIAG == 10 ? t : 0;  // diag 10: ranking skipped (timing only)
@@ -3366,6 +3408,9 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     const int rpb = 256 / G;
     const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
     switch (G) {
+#if MHS_ROW_GMIN < 4
+    case 2: hipLaunchKernelGGL(k_mask_b<2>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+#endif
     case 4: hipLaunchKernelGGL(k_mask_b<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
     case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
     case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
@@ -3394,6 +3439,9 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     const dim3 grid(blocks), blk(256);
 #define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin)
     switch (G) {
+#if MHS_ROW_GMIN < 4
+    case 2: MHS_ANALYZE(2); break;
+#endif
     case 4: MHS_ANALYZE(4); break;
     case 8: MHS_ANALYZE(8); break;
     case 16: MHS_ANALYZE(16); break;
