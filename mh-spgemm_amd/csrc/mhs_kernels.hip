@@ -3403,14 +3403,13 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     // about four chunk iterations per row: a wave then holds several rows, whose
     // dependent load chains overlap (measured on gfx950: 64-lane rows were latency-bound)
     const long long avg = B.M > 0 ? B.nnz / B.M : 0;
-    int G = avg < 4 ? MHS_ROW_GMIN : 8;
+    // rows of < 3 entries (road networks): 2-lane groups, 32 rows per wave (GAP-road-like -3.6 %)
+    int G = avg < 3 ? 2 : avg < 4 ? MHS_ROW_GMIN : 8;
     while (2 * G <= avg / 4 && G < MHS_MASK_GMAX) G <<= 1;
     const int rpb = 256 / G;
     const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
     switch (G) {
-#if MHS_ROW_GMIN < 4
     case 2: hipLaunchKernelGGL(k_mask_b<2>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-#endif
     case 4: hipLaunchKernelGGL(k_mask_b<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
     case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
     case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
