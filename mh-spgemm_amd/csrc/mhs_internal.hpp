@@ -53,16 +53,24 @@ constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so a numeric tiny row spans
 // symbolic (counts only: no segmented sums) sorts every row of at most 8 A entries in
 // 8-lane teams -- eight rows per wave, so one dependent load chain (row -> A -> bmeta -> B)
 // serves eight rows: (8,1) (8,4) (8,8) (32,4).  Numeric keeps its values beside the keys
-// and sums segments per slot, so wide slots cost more: (8,1) (8,4) (32,2) (32,4) (64,4) (64,8).
+// and sums segments per slot, so wide slots cost more: (4,2) (8,4) (32,2) (32,4) (64,4) (64,8).
 // MHS_TINY_SET=0: round 1's classes (8,1) (32,1) (32,2) (32,4) (64,4) (64,8) for both.
 #ifndef MHS_TINY_SET
 #define MHS_TINY_SET 1
 #endif
+#ifndef MHS_TINY0_W4
+#define MHS_TINY0_W4 1  // numeric class 0 as (4,2): 16 rows of <= 4 A entries per wave (GAP-road-like -8 %)
+#endif
+#ifndef MHS_TINYS0_W4
+#define MHS_TINYS0_W4 0  // the same for symbolic class 0
+#endif
 #if MHS_TINY_SET
-__host__ __device__ constexpr int tiny_w(int c) { return c <= 1 ? 8 : c <= 3 ? 32 : 64; }
-__host__ __device__ constexpr int tiny_k(int c) { return c == 0 ? 1 : c == 2 ? 2 : c == 5 ? 8 : 4; }
-__host__ __device__ constexpr int tiny_ws(int c) { return c <= 2 ? 8 : 32; }
-__host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? 1 : c == 2 ? 8 : 4; }
+__host__ __device__ constexpr int tiny_w(int c) { return c == 0 && MHS_TINY0_W4 ? 4 : c <= 1 ? 8 : c <= 3 ? 32 : 64; }
+__host__ __device__ constexpr int tiny_k(int c) {
+    return c == 0 ? (MHS_TINY0_W4 ? 2 : 1) : c == 2 ? 2 : c == 5 ? 8 : 4;
+}
+__host__ __device__ constexpr int tiny_ws(int c) { return c == 0 && MHS_TINYS0_W4 ? 4 : c <= 2 ? 8 : 32; }
+__host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? (MHS_TINYS0_W4 ? 2 : 1) : c == 2 ? 8 : 4; }
 #else
 __host__ __device__ constexpr int tiny_w(int c) { return c == 0 ? 8 : c <= 3 ? 32 : 64; }
 __host__ __device__ constexpr int tiny_k(int c) { return c <= 1 ? 1 : c == 2 ? 2 : c <= 4 ? 4 : 8; }
