@@ -53,7 +53,7 @@ constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so a numeric tiny row spans
 // symbolic (counts only: no segmented sums) sorts every row of at most 8 A entries in
 // 8-lane teams -- eight rows per wave, so one dependent load chain (row -> A -> bmeta -> B)
 // serves eight rows: (8,1) (8,4) (8,8) (32,4).  Numeric keeps its values beside the keys
-// and sums segments per slot, so wide slots cost more: (4,2) (8,4) (32,2) (32,4) (64,4) (64,8).
+// and sums segments per slot, so wide slots cost more: (4,2) (8,4) (16,4) (32,4) (64,4) (64,8).
 // MHS_TINY_SET=0: round 1's classes (8,1) (32,1) (32,2) (32,4) (64,4) (64,8) for both.
 #ifndef MHS_TINY_SET
 #define MHS_TINY_SET 1
@@ -61,13 +61,21 @@ constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so a numeric tiny row spans
 #ifndef MHS_TINY0_W4
 #define MHS_TINY0_W4 1  // numeric class 0 as (4,2): 16 rows of <= 4 A entries per wave (GAP-road-like -8 %)
 #endif
+#ifndef MHS_TINY2_W16
+#define MHS_TINY2_W16 1  // numeric class 2 as (16,4) instead of (32,2) (delaunay-like -12 %, mac_econ-like numeric -9 %)
+#endif
+#ifndef MHS_TINY1_W4
+#define MHS_TINY1_W4 0  // numeric class 1 as (4,8) instead of (8,4)
+#endif
 #ifndef MHS_TINYS0_W4
 #define MHS_TINYS0_W4 0  // the same for symbolic class 0
 #endif
 #if MHS_TINY_SET
-__host__ __device__ constexpr int tiny_w(int c) { return c == 0 && MHS_TINY0_W4 ? 4 : c <= 1 ? 8 : c <= 3 ? 32 : 64; }
+__host__ __device__ constexpr int tiny_w(int c) {
+    return c == 0 && MHS_TINY0_W4 ? 4 : c == 1 && MHS_TINY1_W4 ? 4 : c == 2 && MHS_TINY2_W16 ? 16 : c <= 1 ? 8 : c <= 3 ? 32 : 64;
+}
 __host__ __device__ constexpr int tiny_k(int c) {
-    return c == 0 ? (MHS_TINY0_W4 ? 2 : 1) : c == 2 ? 2 : c == 5 ? 8 : 4;
+    return c == 0 ? (MHS_TINY0_W4 ? 2 : 1) : c == 1 ? (MHS_TINY1_W4 ? 8 : 4) : c == 2 ? (MHS_TINY2_W16 ? 4 : 2) : c == 5 ? 8 : 4;
 }
 __host__ __device__ constexpr int tiny_ws(int c) { return c == 0 && MHS_TINYS0_W4 ? 4 : c <= 2 ? 8 : 32; }
 __host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? (MHS_TINYS0_W4 ? 2 : 1) : c == 2 ? 8 : 4; }
@@ -77,7 +85,7 @@ __host__ __device__ constexpr int tiny_k(int c) { return c <= 1 ? 1 : c == 2 ? 2
 __host__ __device__ constexpr int tiny_ws(int c) { return tiny_w(c); }
 __host__ __device__ constexpr int tiny_ks(int c) { return tiny_k(c); }
 #endif
-constexpr int TINY_FUSED_KMAX = 4;  // largest K of the numeric classes 0..3 (one fused launch)
+constexpr int TINY_FUSED_KMAX = MHS_TINY1_W4 ? 8 : 4;  // largest K of the numeric classes 0..3 (one fused launch)
 // Symbolic uses the classes below TINY_SYM_NC only (past 128 products a hash table
 // counts faster than a sort); numeric uses the 64-lane classes for rows whose table
 // would not fit the small wave bin (measured: cop20k-like 2.3x slower sorted, while
