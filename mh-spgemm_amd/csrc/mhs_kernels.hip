@@ -3419,8 +3419,11 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
 }
 
 // k_analyze: G lanes per row, 256-thread blocks.
+#ifndef MHS_AN_G2
+#define MHS_AN_G2 1  // 2-lane groups for rows of < 3 entries on average (GAP-road-like 5.29 -> 4.97 ms)
+#endif
 static void analyze_geometry(long long nnzA, int M, int* G, int* blocks) {
-    *G = pick_group(nnzA, M, MHS_AN_GMAX);
+    *G = MHS_AN_G2 && M > 0 && nnzA / M < 3 ? 2 : pick_group(nnzA, M, MHS_AN_GMAX);
     const int rpb = 256 / *G;
     *blocks = (M + rpb - 1) / rpb;
 }
@@ -3438,9 +3441,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     const dim3 grid(blocks), blk(256);
 #define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin)
     switch (G) {
-#if MHS_ROW_GMIN < 4
     case 2: MHS_ANALYZE(2); break;
-#endif
     case 4: MHS_ANALYZE(4); break;
     case 8: MHS_ANALYZE(8); break;
     case 16: MHS_ANALYZE(16); break;
