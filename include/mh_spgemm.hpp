@@ -244,9 +244,11 @@ inline void matrix_transposition(const CSR& A, CSR& B, Tool& tools) {
     B.D2H();
 }
 
-inline int readMtxFile(CSR& A, const char* filename) {
+// cache = true: a binary CSR cache beside the file (mhs_read_mtx_cached), re-parsed
+// only when the .mtx changes.
+inline int readMtxFile(CSR& A, const char* filename, bool cache = false) {
     mhs_host_csr h{};
-    const int rc = mhs_read_mtx(filename, &h);
+    const int rc = cache ? mhs_read_mtx_cached(filename, nullptr, &h, nullptr) : mhs_read_mtx(filename, &h);
     if (rc != MHS_OK) {
         std::printf("Could not read Matrix Market file %s.\n", filename);
         return -1;

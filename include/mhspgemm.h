@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 6
+#define MHS_ABI_VERSION 7
 
 typedef enum mhs_status {
     MHS_OK = 0,
@@ -157,6 +157,15 @@ typedef struct mhs_host_csr {
  * duplicates kept; rows sorted by (col, val).  Returns MHS_OK or MHS_ERR_IO. */
 int mhs_read_mtx(const char *path, mhs_host_csr *A);
 void mhs_host_csr_free(mhs_host_csr *A);
+/* Binary CSR cache (replaces re-running the fscanf loop of
+ * inc/mmio_read.h:80-108 on every run).  mhs_read_mtx_cached reads `cache_path`
+ * (NULL: path + ".mhscsr") when its stamp matches the .mtx's size and mtime,
+ * else parses the text with mhs_read_mtx and writes the cache (best effort);
+ * *from_cache (may be NULL) says which.  The cache reader checks ptr/col
+ * invariants and returns MHS_ERR_IO on a truncated or corrupt file. */
+int mhs_read_mtx_cached(const char *path, const char *cache_path, mhs_host_csr *A, int *from_cache);
+int mhs_write_csr_bin(const char *path, const mhs_host_csr *A, int64_t src_size, int64_t src_mtime_ns);
+int mhs_read_csr_bin(const char *path, mhs_host_csr *A, int64_t *src_size, int64_t *src_mtime_ns);
 /* int_result of src/main.cu:102-107. */
 uint64_t mhs_flop_count(int32_t nnzA, const int32_t *Acol, const int32_t *Bptr);
 

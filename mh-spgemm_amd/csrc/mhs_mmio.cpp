@@ -16,7 +16,11 @@
 // and tokenised in parallel chunks; rows are sorted in parallel.
 #include "../../include/mhspgemm.h"
 
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cerrno>
 #include <cstdio>
@@ -66,6 +70,17 @@ struct Entry {
     int r, c;
     double v;
 };
+
+constexpr char kBinMagic[8] = {'M', 'H', 'S', 'C', 'S', 'R', '\0', '\0'};
+constexpr int32_t kBinVersion = 1;
+
+struct BinHeader {
+    char magic[8];
+    int32_t version, M, N, nnz, is_symmetric, pad0;
+    int64_t src_size, src_mtime_ns;
+    int64_t pad1[2];
+};
+static_assert(sizeof(BinHeader) == 64, "binary CSR header is 64 bytes");
 
 }  // namespace
 
@@ -289,6 +304,115 @@ int mhs_read_mtx(const char* path, mhs_host_csr* A) {
             }
         }
     });
+    return MHS_OK;
+}
+
+// ---- binary CSR cache (the text parse of cage15 / wb-edu / GAP-road is
+// the step before the path; inc/mmio_read.h:80-108 re-parses with fscanf on every run).
+// File: a 64-byte header {magic, version, M, N, nnz, is_symmetric, source size, source
+// mtime (ns)}, then ptr[M+1] int32, col[nnz] int32, val[nnz] f64, little-endian as on the
+// host.  The source's size + mtime stamp the cache: a rewritten .mtx invalidates it.
+
+int mhs_write_csr_bin(const char* path, const mhs_host_csr* A, int64_t src_size, int64_t src_mtime_ns) {
+    if (!path || !A || A->M < 0 || A->nnz < 0 || !A->ptr || (A->nnz > 0 && (!A->col || !A->val)))
+        return MHS_ERR_INVALID;
+    BinHeader h{};
+    std::memcpy(h.magic, kBinMagic, sizeof h.magic);
+    h.version = kBinVersion;
+    h.M = A->M;
+    h.N = A->N;
+    h.nnz = A->nnz;
+    h.is_symmetric = A->is_symmetric;
+    h.src_size = src_size;
+    h.src_mtime_ns = src_mtime_ns;
+    // write to a temporary name and rename: a reader never sees a half-written cache
+    const std::string tmp = std::string(path) + ".tmp" + std::to_string((long long)getpid());
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return MHS_ERR_IO;
+    bool ok = fwrite(&h, sizeof h, 1, f) == 1 &&
+              fwrite(A->ptr, sizeof(int32_t), (size_t)A->M + 1, f) == (size_t)A->M + 1 &&
+              (A->nnz == 0 || (fwrite(A->col, sizeof(int32_t), (size_t)A->nnz, f) == (size_t)A->nnz &&
+                               fwrite(A->val, sizeof(double), (size_t)A->nnz, f) == (size_t)A->nnz));
+    ok = (fclose(f) == 0) && ok;
+    if (!ok || rename(tmp.c_str(), path) != 0) {
+        unlink(tmp.c_str());
+        return MHS_ERR_IO;
+    }
+    return MHS_OK;
+}
+
+int mhs_read_csr_bin(const char* path, mhs_host_csr* A, int64_t* src_size, int64_t* src_mtime_ns) {
+    if (!A) return MHS_ERR_INVALID;
+    std::memset(A, 0, sizeof *A);
+    FILE* f = fopen(path, "rb");
+    if (!f) return MHS_ERR_IO;
+    BinHeader h{};
+    if (fread(&h, sizeof h, 1, f) != 1 || std::memcmp(h.magic, kBinMagic, sizeof h.magic) != 0 ||
+        h.version != kBinVersion || h.M < 0 || h.N < 0 || h.nnz < 0) {
+        fclose(f);
+        return MHS_ERR_IO;
+    }
+    const size_t nz = (size_t)h.nnz;
+    A->ptr = (int32_t*)malloc(sizeof(int32_t) * ((size_t)h.M + 1));
+    A->col = (int32_t*)malloc(sizeof(int32_t) * (nz > 0 ? nz : 1));
+    A->val = (double*)malloc(sizeof(double) * (nz > 0 ? nz : 1));
+    bool ok = A->ptr && A->col && A->val &&
+              fread(A->ptr, sizeof(int32_t), (size_t)h.M + 1, f) == (size_t)h.M + 1 &&
+              (nz == 0 || (fread(A->col, sizeof(int32_t), nz, f) == nz &&
+                           fread(A->val, sizeof(double), nz, f) == nz));
+    fclose(f);
+    // a truncated or corrupt cache must not reach the device: check the CSR invariants
+    ok = ok && A->ptr[0] == 0 && A->ptr[h.M] == h.nnz;
+    if (ok) {
+        std::atomic<bool> good{true};
+        parallel_for(h.M, [&](long long lo, long long hi, int) {
+            for (long long r = lo; r < hi && good.load(std::memory_order_relaxed); ++r) {
+                const int32_t s = A->ptr[r], e = A->ptr[r + 1];
+                if (e < s || e > h.nnz) {
+                    good = false;
+                    return;
+                }
+                for (int32_t j = s; j < e; ++j)
+                    if ((uint32_t)A->col[j] >= (uint32_t)h.N) {
+                        good = false;
+                        return;
+                    }
+            }
+        });
+        ok = good.load();
+    }
+    if (!ok) {
+        mhs_host_csr_free(A);
+        return MHS_ERR_IO;
+    }
+    A->M = h.M;
+    A->N = h.N;
+    A->nnz = h.nnz;
+    A->is_symmetric = h.is_symmetric;
+    if (src_size) *src_size = h.src_size;
+    if (src_mtime_ns) *src_mtime_ns = h.src_mtime_ns;
+    return MHS_OK;
+}
+
+int mhs_read_mtx_cached(const char* path, const char* cache_path, mhs_host_csr* A, int* from_cache) {
+    if (!path || !A) return MHS_ERR_INVALID;
+    if (from_cache) *from_cache = 0;
+    struct stat st;
+    if (stat(path, &st) != 0) return MHS_ERR_IO;
+    const int64_t size = (int64_t)st.st_size;
+    const int64_t mtime = (int64_t)st.st_mtim.tv_sec * 1000000000LL + (int64_t)st.st_mtim.tv_nsec;
+    const std::string cache = cache_path && *cache_path ? std::string(cache_path) : std::string(path) + ".mhscsr";
+    int64_t cs = -1, cm = -1;
+    if (mhs_read_csr_bin(cache.c_str(), A, &cs, &cm) == MHS_OK) {
+        if (cs == size && cm == mtime) {
+            if (from_cache) *from_cache = 1;
+            return MHS_OK;
+        }
+        mhs_host_csr_free(A);  // stale: the .mtx changed since the cache was written
+    }
+    const int rc = mhs_read_mtx(path, A);
+    if (rc != MHS_OK) return rc;
+    (void)mhs_write_csr_bin(cache.c_str(), A, size, mtime);  // best effort (read-only dirs)
     return MHS_OK;
 }
 

@@ -1,7 +1,7 @@
 // spgemm_main.cpp -- the `spgemm <file.mtx>` driver (reference src/main.cu:74-217)
 // on top of the C-ABI, printing the reference's stdout lines.
 //
-//   spgemm [--iters K] [--warmup W] [--aat] [--vendor] [--check] [--csv DIR] <file.mtx>
+//   spgemm [--iters K] [--warmup W] [--aat] [--vendor] [--check] [--csv DIR] [--cache] <file.mtx>
 //
 // Flow as in the reference: read (mmio semantics), reject non-square A unless AAT
 // (exit 0, main.cu:92-96), B = A or B = A^T (AAT and not symmetric, :98-101),
@@ -14,6 +14,8 @@
 //   --check   CHECK_RESULT=1: C == vendor C by CSR::operator== -> "pass"/"error" (:186-199)
 //   --csv DIR WRITE=1: append GFLOPS to DIR/Gflops_MH-SpGEMM.csv and, with --vendor,
 //             DIR/Gflops_rocsparse.csv (:173-184, :201-213; the reference's data/)
+//   --cache   read <file.mtx>.mhscsr (binary CSR, stamped with the .mtx's size and
+//             mtime) instead of parsing the text; written on the first run
 // Differences: W untimed warm-up calls (the reference warms the GPU with an
 // empty kernel, MH_spgemm.cuh:10-25), K timed calls averaged with the context's
 // workspace reused between them (the reference's iter/release loop), and an extra
@@ -55,7 +57,7 @@ static void recycle(Tool& tools, CSR& C) {
 
 int main(int argc, char** argv) {
     int iters = 1, warmup = 1;
-    bool aat = false, vendor = false, check = false;
+    bool aat = false, vendor = false, check = false, cache = false;
     std::string csv;
     const char* filename = nullptr;
     bool bad = false;
@@ -66,17 +68,18 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--vendor")) vendor = true;
         else if (!std::strcmp(argv[i], "--check")) check = vendor = true;
         else if (!std::strcmp(argv[i], "--csv") && i + 1 < argc) csv = argv[++i];
+        else if (!std::strcmp(argv[i], "--cache")) cache = true;
         else if (!filename && argv[i][0] != '-') filename = argv[i];
         else bad = true;
     }
     if (bad || !filename || iters < 1 || warmup < 0) {
         std::puts("Invalid Arguments.");
-        std::puts("Usage:\t ./spgemm [--iters K] [--warmup W] [--aat] [--vendor] [--check] [--csv DIR] <Input File>");
+        std::puts("Usage:\t ./spgemm [--iters K] [--warmup W] [--aat] [--vendor] [--check] [--csv DIR] [--cache] <Input File>");
         return -1;
     }
     const std::string matrix_name = extract_matrix_name(filename);
     CSR A, B, C;
-    if (readMtxFile(A, filename) != 0) return -1;
+    if (readMtxFile(A, filename, cache) != 0) return -1;
     if (!aat && A.M != A.N) {
         std::puts("C=AA must have rowA = colA. Exit.");
         return 0;

@@ -102,6 +102,12 @@ def lib() -> ctypes.CDLL:
     L.mhs_read_mtx.restype = c_int
     L.mhs_host_csr_free.argtypes = [P(mhs_host_csr)]
     L.mhs_host_csr_free.restype = None
+    L.mhs_read_mtx_cached.argtypes = [ctypes.c_char_p, ctypes.c_char_p, P(mhs_host_csr), P(c_int)]
+    L.mhs_read_mtx_cached.restype = c_int
+    L.mhs_write_csr_bin.argtypes = [ctypes.c_char_p, P(mhs_host_csr), ctypes.c_int64, ctypes.c_int64]
+    L.mhs_write_csr_bin.restype = c_int
+    L.mhs_read_csr_bin.argtypes = [ctypes.c_char_p, P(mhs_host_csr), P(ctypes.c_int64), P(ctypes.c_int64)]
+    L.mhs_read_csr_bin.restype = c_int
     L.mhs_flop_count.argtypes = [ctypes.c_int32, c_void_p, c_void_p]
     L.mhs_flop_count.restype = ctypes.c_uint64
     L.mhs_memcpy.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int]

@@ -18,6 +18,7 @@ C is allocated by the library.  No torch type crosses the ABI: only pointers.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -411,10 +412,28 @@ def MH_spgemm(A: CSR, B: CSR, C: CSR, timing: Timing, tools: Tool):
     print(f"C.nnz = {C.nnz}")
 
 
-def readMtxFile(A: CSR, filename: str) -> int:
-    """inc/mmio_read.h:34-159 through the library's parallel reader."""
+def readMtxFile(A: CSR, filename: str, cache=None) -> int:
+    """inc/mmio_read.h:34-159 through the library's parallel reader.
+
+    ``cache`` (default ``$MHS_MTX_CACHE``: unset = off, "1" = next to the file,
+    else a directory): read a binary CSR cache stamped with the .mtx's size and
+    mtime instead of the text, writing it on a miss."""
     h = L.mhs_host_csr()
-    rc = L.lib().mhs_read_mtx(str(filename).encode(), ctypes.byref(h))
+    if cache is None:
+        cache = os.environ.get("MHS_MTX_CACHE") or False
+    if cache and cache is not True and str(cache) not in ("1", "true"):
+        d = os.fspath(cache)
+        os.makedirs(d, exist_ok=True)
+        cpath = os.path.join(d, os.path.basename(str(filename)) + ".mhscsr").encode()
+    else:
+        cpath = None
+    if cache:
+        hit = ctypes.c_int(0)
+        rc = L.lib().mhs_read_mtx_cached(str(filename).encode(), cpath, ctypes.byref(h), ctypes.byref(hit))
+        readMtxFile.last_from_cache = bool(hit.value)
+    else:
+        rc = L.lib().mhs_read_mtx(str(filename).encode(), ctypes.byref(h))
+        readMtxFile.last_from_cache = False
     if rc != L.MHS_OK:
         print(f"Could not read Matrix Market file {filename}.")
         return -1

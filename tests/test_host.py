@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.lib_path()], capture_output=True, text=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert set(names) <= exported
-    assert L.mhs_abi_version() == 6
+    assert L.mhs_abi_version() == 7
 
 
 def test_vendor_library_exports_every_declared_symbol():
@@ -86,6 +86,56 @@ def test_product_reader_large_parallel_parse(tmp_path):
     assert mhspgemm.readMtxFile(A, str(f)) == 0
     M2, N2, p, col, val, _ = orc.read_mtx(f)
     assert np.array_equal(A.ptr, p) and np.array_equal(A.col, col) and np.array_equal(A.val, val)
+
+
+def test_binary_csr_cache(tmp_path):
+    # the first cached read parses the text and writes <file>.mhscsr; the
+    # second reads the cache (bit-identical); rewriting the .mtx invalidates it; a
+    # corrupt cache is refused and re-parsed from the text.
+    import os
+    rng = np.random.default_rng(3)
+    M, nz = 300, 2000
+    lines = ["%%MatrixMarket matrix coordinate real symmetric", f"{M} {M} {nz}"]
+    lines += [f"{a} {b} {float(x)!r}" for a, b, x in
+              zip(rng.integers(1, M + 1, nz), rng.integers(1, M + 1, nz), rng.standard_normal(nz))]
+    f = tmp_path / "m.mtx"
+    f.write_text("\n".join(lines) + "\n")
+    ref = mhspgemm.CSR()
+    assert mhspgemm.readMtxFile(ref, str(f)) == 0
+
+    def read():
+        A = mhspgemm.CSR()
+        assert mhspgemm.readMtxFile(A, str(f), cache=True) == 0
+        assert (A.M, A.N, A.nnz, A.isSymmetric) == (ref.M, ref.N, ref.nnz, ref.isSymmetric)
+        assert np.array_equal(A.ptr, ref.ptr) and np.array_equal(A.col, ref.col)
+        assert np.array_equal(A.val.view(np.uint64), ref.val.view(np.uint64))
+        return mhspgemm.readMtxFile.last_from_cache
+
+    cache = tmp_path / "m.mtx.mhscsr"
+    assert read() is False and cache.exists()
+    assert read() is True
+    # a changed .mtx (new mtime) is re-parsed, never served from the old cache
+    st = os.stat(f)
+    os.utime(f, ns=(st.st_atime_ns, st.st_mtime_ns + 10**9))
+    assert read() is False
+    assert read() is True
+    # truncated / corrupt caches are refused by the binary reader, the text is parsed again
+    data = cache.read_bytes()
+    cache.write_bytes(data[: len(data) - 8])
+    assert read() is False
+    blob = bytearray(cache.read_bytes())
+    col_off = 64 + 4 * (M + 1)
+    blob[col_off:col_off + 4] = np.int32(M + 5).tobytes()  # column out of range
+    cache.write_bytes(bytes(blob))
+    h = _lib.mhs_host_csr()
+    assert _lib.lib().mhs_read_csr_bin(str(cache).encode(), ctypes.byref(h), None, None) == _lib.MHS_ERR_IO
+    assert read() is False
+    # a cache directory instead of the file's own
+    d = tmp_path / "cachedir"
+    A = mhspgemm.CSR()
+    assert mhspgemm.readMtxFile(A, str(f), cache=str(d)) == 0 and (d / "m.mtx.mhscsr").exists()
+    assert mhspgemm.readMtxFile(A, str(f), cache=str(d)) == 0 and mhspgemm.readMtxFile.last_from_cache
+    assert np.array_equal(A.col, ref.col)
 
 
 def test_reader_errors(tmp_path):
