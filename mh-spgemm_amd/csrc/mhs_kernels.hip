@@ -434,6 +434,32 @@ struct WaveQueue {
     }
 };
 
+#ifndef MHS_BLKQ
+#define MHS_BLKQ 1  // block-per-row walks (k_sym_rare, k_num_block) take rows from one global cursor
+#endif
+#ifndef MHS_BLKQ_NUM
+#define MHS_BLKQ_NUM MHS_BLKQ
+#endif
+#ifndef MHS_BLKQ_SYMB
+#define MHS_BLKQ_SYMB 0  // k_sym_block<256> too: measured cant-s1-like symbolic +12 %, scircuit-like +12 %
+#endif              // (tens of thousands of uniform rows: one cursor contended, the static walk balanced)
+// Dynamic row queue of a block team: thread 0 takes the next list index from the launch's
+// cursor (one atomic per row: the block bins hold hundreds to a few thousand rows), the
+// block reads it between two barriers.  Power-law rows differ by orders of magnitude in
+// cost; a static stride left the kernel's end to the block that drew the heaviest rows.
+struct BlockQueue {
+    int* cur;
+    int* slot;  // an LDS word
+    int count;
+    __device__ bool next(int& idx) const {
+        __syncthreads();  // every thread has read the previous index
+        if (threadIdx.x == 0) *slot = atomicAdd(cur, 1);
+        __syncthreads();
+        idx = *slot;
+        return idx < count;
+    }
+};
+
 // ------------------------------------------------------------------- teams ---
 // A team processes one row at a time: a wave (64 lanes, wave_sync) or a whole
 // block (__syncthreads; reductions through an LDS header).  GlobalTeam is a
@@ -1958,6 +1984,13 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
     const int count = a.stats->sym_count[a.bin];
     const int* list = a.list + (long long)(a.bin - 1) * a.M;
     int4* stage = (int4*)(smem + 1024);
+    if (MHS_BLKQ_SYMB) {
+        if (count == 0) return;  // (launched before the bin sizes are known: most calls have none)
+        __shared__ int qslot;
+        const BlockQueue q{a.cursors + (NUM_NB + a.bin) * 8 * CURSOR_STRIDE, &qslot, count};
+        for (int li; q.next(li);) sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[li]), E, stage);
+        return;
+    }
     for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
 }
@@ -2094,17 +2127,25 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
     int4* stage = (int4*)(smem + 1024);
     BlockTeam<1024, false> tm{(long long*)smem};
     TileEntry* E = (TileEntry*)(smem + BLOCK_HDR);
+    __shared__ int qslot;
 #pragma unroll 1
     for (int bin = SYM_GLOBAL; bin >= SYM_B1024; --bin) {
         const int count = a.stats->sym_count[bin];
         const int* list = a.list + (long long)(bin - 1) * a.M;
-        for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride) {
-            const int row = __builtin_amdgcn_readfirstlane(list[rw.first]);
+        auto one = [&](int li) {
+            const int row = __builtin_amdgcn_readfirstlane(list[li]);
             const int span = __builtin_amdgcn_readfirstlane(a.rhi[row]) - __builtin_amdgcn_readfirstlane(a.rlo[row]) + 1;
             if (bin == SYM_B1024 && sym_direct(span, __builtin_amdgcn_readfirstlane(a.rtflop[row])))
                 sym_row(tm, a, row, E, stage);
             else if (!(MHS_SPANRANK && sym_row_bitmap(tm, a, row, (char*)E, stage)))
                 sym_row_wide(tm, a, row, (unsigned long long*)E, stage, (int*)(smem + 512));
+        };
+        if (count == 0) continue;  // (no atomics for an empty bin: most matrices have none)
+        if (MHS_BLKQ) {
+            const BlockQueue q{a.cursors + (NUM_NB + bin) * 8 * CURSOR_STRIDE, &qslot, count};
+            for (int li; q.next(li);) one(li);
+        } else {
+            for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride) one(rw.first);
         }
     }
     __syncthreads();  // phase 2 reuses the whole LDS
@@ -2113,6 +2154,8 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
     const int count = a.stats->sym_count[SYM_WM];
     const int* list = a.list + (long long)(SYM_WM - 1) * a.M;
     WaveTeam wt;
+    // (a row queue here -- one atomic per wave and row on one cursor -- measured +40-95 µs
+    // per call on cant / cop20k / scircuit-like: 4096 waves contending; static walk kept)
     for (RowWalk rw(count, 16, w); rw.first < rw.end; rw.first += rw.stride)
         sym_row(wt, a, __builtin_amdgcn_readfirstlane(list[rw.first]), Ew, nullptr);
 }
@@ -3035,8 +3078,18 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
     char* reg = GLOBALMEM ? (a.gscratch + (long long)blockIdx.x * a.gbytes) : (smem + BLOCK_HDR);
     int* counter = (int*)(smem + 128);
     int4* stage = (int4*)(smem + 1024);
-    for (RowWalk rw(a.count, 1, 0); rw.first < rw.end; rw.first += rw.stride) {
-        const int row = __builtin_amdgcn_readfirstlane(a.list[rw.first]);
+    __shared__ int qslot;
+    const BlockQueue q{a.cursor, &qslot, a.count};
+    RowWalk rw(a.count, 1, 0);
+    for (int li;;) {
+        if (MHS_BLKQ_NUM) {
+            if (!q.next(li)) break;
+        } else {
+            if (rw.first >= rw.end) break;
+            li = rw.first;
+            rw.first += rw.stride;
+        }
+        const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
         if constexpr (T == 1024 && !GLOBALMEM) {
             const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
             const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
@@ -3502,17 +3555,19 @@ hipError_t probe_counter(unsigned long long** dev) {
 
 hipError_t init_kernel_attributes() {
     // gfx950 grants up to 160 KiB of LDS per workgroup; make the large dynamic
-    // requests explicit for the block-per-row kernels (which use no static LDS).
+    // requests explicit for the block-per-row kernels.  k_sym_rare and k_num_block hold a
+    // static LDS word (the row queue) and launch with at most LDS_MAX - 1024 dynamic bytes:
+    // static + dynamic must stay within the 160 KiB or the attribute call fails.
     hipError_t e = hipFuncSetAttribute((const void*)k_sym_block<1024, false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX - 1024);
     if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_sym_rare, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+        e = hipFuncSetAttribute((const void*)k_sym_rare, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX - 1024);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_num_block<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                LDS_MAX);
+                                LDS_MAX - 1024);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_num_block<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                LDS_MAX);
+                                LDS_MAX - 1024);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_num_wave_direct<NUM_W16_BYTES>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
