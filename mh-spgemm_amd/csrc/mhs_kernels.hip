@@ -405,6 +405,12 @@ struct RowWalk {
 #ifndef MHS_DYN
 #define MHS_DYN 0  // > 0: wave bins take MHS_DYN consecutive list entries at a time from a cursor
 #endif
+#ifndef MHS_GUIDED16
+#define MHS_GUIDED16 1  // guided walk (see num_wave_rows) in the numeric 16 KiB bins: 1 hash, 2 direct/grouped
+#endif
+#ifndef MHS_GUIDED_STATIC
+#define MHS_GUIDED_STATIC 4  // eighths of an XCD group's rows walked statically before the cursor
+#endif
 // Dynamic XCD-grouped walk: group g = blockIdx % 8 (an XCD under round-robin dispatch) owns
 // the g-th eighth of the list; its waves take CH consecutive entries at a time from the
 // group's cursor, in list order.  The rows in flight on an XCD stay one compact window
@@ -3046,7 +3052,31 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
             num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH>(tm, a, row, reg + WAVE_HDR,
                                                                              (int*)reg, nullptr);
     };
-    if (MHS_DYN > 0) {
+    // The 16 KiB bins hold the heaviest wave rows (power-law rows of hundreds of tiles, a
+    // few rows per wave): a static stride leaves the launch's end to the wave that drew the
+    // heaviest ones.  Guided walk: each XCD group's waves stride statically through the first
+    // MHS_GUIDED_STATIC/8 of its eighth of the list (row locality, no atomics), then take the
+    // rest one row at a time from the group's cursor.  Measured (profiles/r02p_guided): hash
+    // bin guided with half static: wb-edu-like numeric -4 %, webbase-like -2 %, cage15-like and
+    // pdb1HYS-like neutral; the whole bin from the cursor (2 rows a take): wb-edu -12 %,
+    // webbase -10 %, but cage15 +3.5 %; the direct / grouped 16 KiB bins guided: pdb1HYS +10 %.
+    constexpr bool guided = MHS_DYN == 0 && BYTES == NUM_W16_BYTES &&
+                            ((HASH && (MHS_GUIDED16 & 1)) || (!HASH && (MHS_GUIDED16 & 2)));
+    if (guided && (gridDim.x & 7) == 0) {
+        const int g = (int)(blockIdx.x & 7);
+        const int begin = (int)((long long)a.count * g / 8), end = (int)((long long)a.count * (g + 1) / 8);
+        const int split = begin + (int)((long long)(end - begin) * MHS_GUIDED_STATIC / 8);
+        const int stride = (int)(gridDim.x >> 3) * WPB;
+        for (int li = begin + (int)(blockIdx.x >> 3) * WPB + w; li < split; li += stride) one(li);
+        int* cur = a.cursor + g * CURSOR_STRIDE;
+        for (;;) {
+            int t = 0;
+            if (lane_id() == 0) t = atomicAdd(cur, 1);
+            const int li = split + __builtin_amdgcn_readfirstlane(t);
+            if (li >= end) break;
+            one(li);
+        }
+    } else if (MHS_DYN > 0) {
         WaveQueue q(a.cursor, a.count, MHS_DYN);
         for (int li; q.next(li);) one(li);
     } else {
