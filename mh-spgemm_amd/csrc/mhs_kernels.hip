@@ -408,6 +408,9 @@ struct RowWalk {
 #ifndef MHS_GUIDED16
 #define MHS_GUIDED16 1  // guided walk (see num_wave_rows) in the numeric 16 KiB bins: 1 hash, 2 direct/grouped
 #endif
+#ifndef MHS_DYN16_MAX
+#define MHS_DYN16_MAX 32768  // hash 16 KiB bins of at most this many rows: all rows from the cursor
+#endif
 #ifndef MHS_GUIDED_STATIC
 #define MHS_GUIDED_STATIC 4  // eighths of an XCD group's rows walked statically before the cursor
 #endif
@@ -2501,6 +2504,7 @@ struct NumArgs {
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
     int* cursor;             // this launch's 8 row cursors (MHS_DYN)
     SpillLists sp;           // tile lists of rows past the row cache's cap (symbolic -> numeric)
+    int qall;                // guided bins: every row from the cursor (few rows a wave)
 };
 
 #ifndef MHS_RANK_SORT
@@ -3062,7 +3066,10 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     // webbase -10 %, but cage15 +3.5 %; the direct / grouped 16 KiB bins guided: pdb1HYS +10 %.
     constexpr bool guided = MHS_DYN == 0 && BYTES == NUM_W16_BYTES &&
                             ((HASH && (MHS_GUIDED16 & 1)) || (!HASH && (MHS_GUIDED16 & 2)));
-    if (guided && (gridDim.x & 7) == 0) {
+    if (guided && a.qall) {
+        WaveQueue q(a.cursor, a.count, 1);
+        for (int li; q.next(li);) one(li);
+    } else if (guided && (gridDim.x & 7) == 0) {
         const int g = (int)(blockIdx.x & 7);
         const int begin = (int)((long long)a.count * g / 8), end = (int)((long long)a.count * (g + 1) / 8);
         const int split = begin + (int)((long long)(end - begin) * MHS_GUIDED_STATIC / 8);
@@ -3765,7 +3772,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         return ss[k];
     };
     hipStream_t s = ss[0];
-    NumArgs a;
+    NumArgs a{};
     a.dense_span_max = dense_span_max;
     a.mcache = w.mcache;
     a.mc_list = w.mc_list;
@@ -3859,9 +3866,11 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         const int count = a.count = h.num_count[NUM_W16H];
         a.list = w.bin_list + (long long)(NUM_W16H - 1) * A.M;
         a.cursor = w.cursors + NUM_W16H * 8 * CURSOR_STRIDE;
+        a.qall = count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
         s = next_stream();
         hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), dim3(round8((count + WPB - 1) / WPB, 2048)),
                            dim3(256), WPB * NUM_W16_BYTES, s, a);
+        a.qall = 0;
     }
     if (h.num_count[NUM_WSH] > 0) {
         const int count = a.count = h.num_count[NUM_WSH];
