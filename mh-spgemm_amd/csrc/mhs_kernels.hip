@@ -408,6 +408,10 @@ struct RowWalk {
 #ifndef MHS_GUIDED16
 #define MHS_GUIDED16 1  // guided walk (see num_wave_rows) in the numeric 16 KiB bins: 1 hash, 2 direct/grouped
 #endif
+#ifndef MHS_GRP_CHUNK
+#define MHS_GRP_CHUNK 63  // A entries staged per chunk in the grouped walk (<= 64)
+#endif
+static_assert(MHS_GRP_CHUNK >= 1 && MHS_GRP_CHUNK <= 64, "a chunk is one entry per lane");
 #ifndef MHS_DYN16_MAX
 #define MHS_DYN16_MAX 32768  // hash 16 KiB bins of at most this many rows: all rows from the cursor
 #endif
@@ -1254,13 +1258,16 @@ __device__ __forceinline__ void for_products_group(int a0, int a1, const int* __
     constexpr int RM = RG_MAX;
     static_assert(MHS_RUN_MAX <= 3, "grouped walks merge runs of up to 3 B rows");
     const int lane = lane_id();
-    for (int jb = a0; jb < a1; jb += 64) {
-        const StagedChunk x = stage_chunk(lane, jb, a1, Acol, Aval, bmeta, false);
+    // chunks of MHS_GRP_CHUNK entries: 63 keeps the 3-entry runs of dof-3 rows whole (a chunk
+    // edge cuts a run: a 1-entry visit in one chunk, a 2-entry one in the next, masked sweeps)
+    for (int jb = a0; jb < a1; jb += MHS_GRP_CHUNK) {
+        const int ce = min(a1, jb + MHS_GRP_CHUNK);
+        const StagedChunk x = stage_chunk(lane, jb, ce, Acol, Aval, bmeta, false);
         const int jl = jb + lane;
         double avr[RM];
         avr[0] = x.av;
 #pragma unroll
-        for (int r = 1; r < RM; ++r) avr[r] = (jl < a1 && r < R) ? Aval[jl + r * nA] : 0.0;
+        for (int r = 1; r < RM; ++r) avr[r] = (jl < ce && r < R) ? Aval[jl + r * nA] : 0.0;
         const int G = (x.lmax > 1 && Grow < MHS_RUN_GMIN) ? MHS_RUN_GMIN : Grow;
         const int gs = 31 - __clz(G);
         const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
