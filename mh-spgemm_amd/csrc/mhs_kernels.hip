@@ -412,6 +412,9 @@ struct RowWalk {
 #define MHS_GRP_CHUNK 63  // A entries staged per chunk in the grouped walk (<= 64)
 #endif
 static_assert(MHS_GRP_CHUNK >= 1 && MHS_GRP_CHUNK <= 64, "a chunk is one entry per lane");
+#ifndef MHS_SYMWM_DYN_MAX
+#define MHS_SYMWM_DYN_MAX 32768  // k_sym_rare's 10 KiB wave rows from the cursors up to this many rows
+#endif
 #ifndef MHS_DYN16_MAX
 #define MHS_DYN16_MAX 32768  // hash 16 KiB bins of at most this many rows: all rows from the cursor
 #endif
@@ -2170,8 +2173,15 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
     const int count = a.stats->sym_count[SYM_WM];
     const int* list = a.list + (long long)(SYM_WM - 1) * a.M;
     WaveTeam wt;
-    // (a row queue here -- one atomic per wave and row on one cursor -- measured +40-95 µs
-    // per call on cant / cop20k / scircuit-like: 4096 waves contending; static walk kept)
+    // A bin of a few rows per wave (<= MHS_SYMWM_DYN_MAX) takes them from the XCD groups'
+    // cursors: blocks leave phase 1 at different times, and the early ones' waves then take
+    // the rows the late ones would have held.  (Every wave on one cursor, every call, even
+    // an empty bin's: +40-95 µs per call on cant / cop20k / scircuit-like -- measured.)
+    if (count > 0 && count <= MHS_SYMWM_DYN_MAX) {
+        WaveQueue q(a.cursors + (NUM_NB + SYM_WM) * 8 * CURSOR_STRIDE, count, 1);
+        for (int li; q.next(li);) sym_row(wt, a, __builtin_amdgcn_readfirstlane(list[li]), Ew, nullptr);
+        return;
+    }
     for (RowWalk rw(count, 16, w); rw.first < rw.end; rw.first += rw.stride)
         sym_row(wt, a, __builtin_amdgcn_readfirstlane(list[rw.first]), Ew, nullptr);
 }
