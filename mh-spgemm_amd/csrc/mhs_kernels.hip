@@ -61,7 +61,7 @@
 #define MHS_TILE_GMIN 4  // narrowest lane group of a tile walk
 #endif
 #ifndef MHS_RUN_GMIN
-#define MHS_RUN_GMIN 32  // narrowest lane group of a chunk with merged runs
+#define MHS_RUN_GMIN 8  // narrowest lane group of a chunk with merged runs (32 before: see DESIGN §8)
 #endif
 #ifndef MHS_MASK_GMAX
 #define MHS_MASK_GMAX 64
