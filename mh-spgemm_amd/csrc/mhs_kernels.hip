@@ -52,8 +52,11 @@
 #define MHS_UNROLL_BLOCK 8  // ... in the block kernels (measured: S1-like rows -9%; the wave kernels keep 4)
 #endif
 #ifndef MHS_NUM_WS_GRID
-#define MHS_NUM_WS_GRID 4096  // block cap of the small-row numeric launch
+#define MHS_NUM_WS_GRID 4096  // block cap of the small-row grouped numeric launch
 #endif
+#ifndef MHS_NUM_WSX_GRID
+#define MHS_NUM_WSX_GRID 8192  // ... of the small-row hash / direct launches (4096: cage15-like numeric +9 %,
+#endif                         // cant-perturbed +5 %; the grouped launch: 8192 measured +1.4 % on cant-like)
 #ifndef MHS_VAL_GMIN
 #define MHS_VAL_GMIN 4  // narrowest lane group of a value walk
 #endif
@@ -3894,7 +3897,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         a.list = w.bin_list + (long long)(NUM_WSH - 1) * A.M;
         a.cursor = w.cursors + NUM_WSH * 8 * CURSOR_STRIDE;
         s = next_stream();
-        hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
+        hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WSX_GRID)),
                            dim3(256), WPB * NUM_WS_BYTES, s, a);
     }
     if (h.num_count[NUM_W16] > 0) {
@@ -3967,7 +3970,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         a.list = w.bin_list + (long long)(NUM_WS - 1) * A.M;
         a.cursor = w.cursors + NUM_WS * 8 * CURSOR_STRIDE;
         s = next_stream();
-        hipLaunchKernelGGL(k_num_wave_direct<NUM_WS_BYTES>, dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
+        hipLaunchKernelGGL(k_num_wave_direct<NUM_WS_BYTES>, dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WSX_GRID)),
                            dim3(256), WPB * NUM_WS_BYTES, s, a);
     }
     return used;
