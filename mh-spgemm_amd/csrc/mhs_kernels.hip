@@ -54,6 +54,12 @@
 #ifndef MHS_NUM_WS_GRID
 #define MHS_NUM_WS_GRID 4096  // block cap of the small-row grouped numeric launch
 #endif
+#ifndef MHS_TINY64_GRID
+#define MHS_TINY64_GRID 4096  // block cap of the 64-lane tiny numeric launches (8192: wb-edu-like +6 %)
+#endif
+#ifndef MHS_NUM_W16H_GRID
+#define MHS_NUM_W16H_GRID 2048  // block cap of the 16 KiB hash launch (4096: neutral, profiles/r02za2_grid)
+#endif
 #ifndef MHS_NUM_WSX_GRID
 #define MHS_NUM_WSX_GRID 8192  // ... of the small-row hash / direct launches (4096: cage15-like numeric +9 %,
 #endif                         // cant-perturbed +5 %; the grouped launch: 8192 measured +1.4 % on cant-like)
@@ -3653,7 +3659,7 @@ size_t sym_global_bytes_per_block(int N) {
 // Numeric tiny class c, `rows` rows.
 static void launch_tiny_num(int c, int rows, const TinyArgs& t, hipStream_t s) {
 #define MHS_TINY(WW, KK)                                                                                  \
-    hipLaunchKernelGGL((k_tiny_num<WW, KK>), dim3(round8((rows + 256 / (WW) - 1) / (256 / (WW)), 4096)), \
+    hipLaunchKernelGGL((k_tiny_num<WW, KK>), dim3(round8((rows + 256 / (WW) - 1) / (256 / (WW)), MHS_TINY64_GRID)), \
                        dim3(256), 256 * (KK) * 8, s, t)
     switch (c) {
     case 0: MHS_TINY(tiny_w(0), tiny_k(0)); break;
@@ -3888,7 +3894,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         a.cursor = w.cursors + NUM_W16H * 8 * CURSOR_STRIDE;
         a.qall = count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
         s = next_stream();
-        hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), dim3(round8((count + WPB - 1) / WPB, 2048)),
+        hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_W16H_GRID)),
                            dim3(256), WPB * NUM_W16_BYTES, s, a);
         a.qall = 0;
     }
