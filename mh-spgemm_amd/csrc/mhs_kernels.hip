@@ -61,7 +61,7 @@
 #define MHS_NUM_W16H_GRID 2048  // block cap of the 16 KiB hash launch (4096: neutral, profiles/r02za2_grid)
 #endif
 #ifndef MHS_NUM_WSX_GRID
-#define MHS_NUM_WSX_GRID 8192  // ... of the small-row hash / direct launches (4096: cage15-like numeric +9 %,
+#define MHS_NUM_WSX_GRID 16384  // ... of the small-row hash / direct launches (8192: cage15-like numeric +4.5 %, 4096: +13 %,
 #endif                         // cant-perturbed +5 %; the grouped launch: 8192 measured +1.4 % on cant-like)
 #ifndef MHS_VAL_GMIN
 #define MHS_VAL_GMIN 4  // narrowest lane group of a value walk
