@@ -54,12 +54,16 @@ for p in (str(ROOT), str(ROOT / "mh-spgemm_amd")):
 import numpy as np  # noqa: E402
 
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+# numeric tiny classes (W lanes x K products per row; mirrors tiny_w / tiny_k of
+# mh-spgemm_amd/csrc/mhs_internal.hpp): numeric bins NUM_TINY + c, c = 0..5
+TINY_WK = [(4, 2), (8, 4), (16, 4), (32, 4), (64, 4), (64, 8)]
 # numeric bin id -> kernel (mhs_internal.hpp NumBin; include/mhspgemm.h num_bins)
-NUM_BIN_KERNELS = ["", "k_num_wave_direct<5120>", "k_num_wave_direct<16384>", "k_num_block<256>",
-                   "k_num_block<1024>", "k_num_block<1024,global>", "k_num_wave<10240,grouped>",
-                   "k_num_wave<16384,grouped>", "k_tiny_num_small(8x1)", "k_tiny_num_small(32x1)",
-                   "k_tiny_num_small(32x2)", "k_tiny_num_small(32x4)", "k_tiny_num<64,4>", "k_tiny_num<64,8>",
-                   "k_num_wave_hash<5120>", "k_num_wave_hash<16384>"]
+NUM_BIN_KERNELS = (["", "k_num_wave_direct<5120>", "k_num_wave_direct<16384>", "k_num_block<256>",
+                    "k_num_block<1024>", "k_num_block<1024,global>", "k_num_wave<10240,grouped>",
+                    "k_num_wave<16384,grouped>"]
+                   + [f"k_tiny_num_small({w}x{k}) (numeric-first rows: k_tiny_copy_rows)" if w <= 32
+                      else f"k_tiny_num<{w},{k}>" for w, k in TINY_WK]
+                   + ["k_num_wave_hash<5120>", "k_num_wave_hash<16384>"])
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -74,7 +78,8 @@ def b_comp(M, nnzA, nnzC, nnzB_extra=0, MB_extra=0):
     return 8 * (M + 1) + 12 * nnzA + 12 * nnzC + 12 * nnzB_extra + 4 * MB_extra
 
 
-NUMERIC_PREFIXES = ("k_num_", "k_tiny_num")
+# every kernel of the numeric phase: the bins' kernels and the numeric-first rows' slot copy
+NUMERIC_PREFIXES = ("k_num_", "k_tiny_num", "k_tiny_copy")
 
 
 def pmc_traffic(matrix: str):
@@ -95,9 +100,26 @@ def pmc_traffic(matrix: str):
         return None, None, None
 
 
+def host_cpu():
+    """(nproc, CPU model) of this host (the core count and lscpu model are stated)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        nproc = os.cpu_count() or 1
+    return nproc, model
+
+
 def cpu_baseline(A, budget_s: float = 12.0):
-    """Oracle (C restatement of the reference path) on the same workload,
-    every host core; repeats until ~budget_s of CPU work, median."""
+    """Oracle (C restatement of the reference path) on the same workload, on the
+    threads OpenMP gives it; repeats until ~budget_s of CPU work, median."""
     from oracle import oracle as orc
     threads = orc.max_threads()
     times = []
@@ -120,7 +142,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--matrix", default="cant")
+    ap.add_argument("--matrix", default=None,
+                    help="default: cant (BASELINE configs[1]) on 1 GPU, cage15 (configs[4], row-sharded) on N > 1")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--gather", action="store_true", help="N>1: also time the gatherv of C to rank 0")
     ap.add_argument("--exchange", default="halo", choices=["halo", "full"],
@@ -145,8 +168,22 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
-    A, source = synth.load_or_synth(args.matrix)
-    flop = mhspgemm.flop_count_np(A.col, A.ptr)
+    if args.matrix is None:
+        args.matrix = "cant" if world == 1 else "cage15"
+    if world == 1:
+        A, source = synth.load_or_synth(args.matrix)
+        M_glob, nnzA = A.M, A.nnz
+        flop = mhspgemm.flop_count_np(A.col, A.ptr)
+    else:
+        # one host copy per node: local rank 0 writes the matrix once as .npy files, every
+        # rank memory-maps them and copies out only its row block (no rank holds a private
+        # copy of the whole matrix)
+        if local == 0:
+            synth.build_shared(args.matrix)
+        dist.barrier()
+        M_glob, N_glob, s_ptr, s_col, s_val, source = synth.open_shared(args.matrix)
+        nnzA = int(s_ptr[-1])
+        flop = mhspgemm.flop_count_np(s_col, s_ptr) if rank == 0 else 0
     tool = mhspgemm.Tool(local)
     tool.set_stream(torch.cuda.current_stream(local).cuda_stream)
     dev = f"cuda:{local}"
@@ -201,14 +238,39 @@ def main():
     else:
         from mhspgemm import distributed as D
         from mhspgemm import _lib as L
+        # the same matrix on ONE GPU first (rank 0, the other ranks wait): the speed-up of
+        # this line is computed on one workload
+        one_gpu = None
+        if rank == 0:
+            A1 = mhspgemm.CSR(M_glob, N_glob, np.array(s_ptr), np.array(s_col), np.array(s_val))
+            A1.H2D(local)
+            t1 = mhspgemm.Tool(local)
+            t1.set_stream(torch.cuda.current_stream(local).cuda_stream)
+            t1.set_option(L.MHS_OPT_SYNC, 0)
+            for _ in range(args.warmup):
+                C, _ = mhspgemm.spgemm(t1, A1, A1, timing=False)
+                C.release()
+            torch.cuda.synchronize(local)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                C, _ = mhspgemm.spgemm(t1, A1, A1, timing=False)
+                C.release()
+            torch.cuda.synchronize(local)
+            ms1 = (time.perf_counter() - t0) / args.steps * 1e3
+            one_gpu = {"ms_per_step": round(ms1, 4), "value": round(2.0 * flop / (ms1 * 1e-3) / 1e9, 2),
+                       "note": "the same matrix, whole, on rank 0's GPU alone (same steps / warmup)"}
+            t1.close()
+            A1.release()
+            del A1
+            torch.cuda.empty_cache()
+        barrier()
         tool.set_option(L.MHS_OPT_SYNC, 0)  # stream-ordered calls: no host wait after the numeric launch
         # each rank keeps only its equal-row block of the input (what a rank reading its part
         # of the file would hold); the flop balance and the exchange plan are built from the
         # blocks with collectives, timed as plan_ms (setup, outside the steps)
-        r0, r1 = D.equal_rows(A.M, world, rank)
-        eq = D.local_block(A.ptr, A.col, A.val, r0, r1, dev)
-        M_glob = A.M
-        A.release()
+        r0, r1 = D.equal_rows(M_glob, world, rank)
+        eq = D.local_block(s_ptr, s_col, s_val, r0, r1, dev)
+        del s_col, s_val
         barrier()
         p0 = time.perf_counter()
         blk = D.rebalance(eq, M_glob)
@@ -260,7 +322,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    balg = b_alg(A.M, A.nnz, flop, nnzC)
+    balg = b_alg(M_glob, nnzA, flop, nnzC)
     out = {
         "metric": METRIC,
         "value": round(gflops, 2),
@@ -276,7 +338,7 @@ def main():
         "data": "synthetic" if source.startswith("synthetic") else "file",
         "config": {
             "workload": f"{args.matrix}.mtx A*A ({source}), device-resident A -> device-resident sorted C",
-            "matrix": args.matrix, "rows": A.M, "nnzA": A.nnz, "flop": flop, "nnzC": nnzC,
+            "matrix": args.matrix, "rows": M_glob, "nnzA": nnzA, "flop": flop, "nnzC": nnzC,
             "parallelism": "single GPU" if N_GPUS == 1 else
                            f"row-sharded x{N_GPUS}, {args.exchange} exchange of B's rows in every step, C distributed",
             "memory": "steady-state steps reuse the context's workspace and pooled C buffers "
@@ -285,7 +347,7 @@ def main():
     }
     if N_GPUS == 1:
         avg_num = float(np.mean(numeric_ms))
-        bc = b_comp(A.M, A.nnz, nnzC)
+        bc = b_comp(M_glob, nnzA, nnzC)
         achieved = bc / (avg_num * 1e-3) / 1e9
         traffic, tsrc, tkern = pmc_traffic(args.matrix)
         nk = [k for k, c in zip(NUM_BIN_KERNELS, phases[-1].num_bins) if c > 0 and k]
@@ -309,15 +371,19 @@ def main():
         ph["t_ref_getTotal"] = round(float(np.mean([p.getTotal() for p in phases])), 4)
         ph["note"] = "5 synchronised calls with per-phase events, after the timed region"
         out["phases_ms"] = ph
-        out["bins"] = {"symbolic": phases[-1].sym_bins[:6], "numeric": phases[-1].num_bins[:9]}
+        out["bins"] = {"symbolic": phases[-1].sym_bins[:12], "numeric": phases[-1].num_bins[:16],
+                       "numeric_kernels": {NUM_BIN_KERNELS[i]: c for i, c in enumerate(phases[-1].num_bins[:16])
+                                           if i and c}}
         if not args.no_cpu:
             med, threads, reps, one = cpu_baseline(A)
+            nproc, model = host_cpu()
             out["cpu_baseline"] = {
                 "value": round(2.0 * flop / med / 1e9, 3), "unit": "GFLOPS", "cores": threads,
                 "kind": "port",
                 "sample": f"full {args.matrix} A*A (symbolic+numeric, Gustavson, oracle/), median of {reps} "
-                          f"runs of {med*1e3:.1f} ms on {threads} threads; 1 thread: "
+                          f"runs of {med*1e3:.1f} ms on {threads} OpenMP threads; 1 thread: "
                           f"{2.0 * flop / one / 1e9:.3f} GFLOPS ({one*1e3:.0f} ms)",
+                "host": {"nproc": nproc, "cpu_model": model, "omp_threads": threads},
             }
         else:
             out["cpu_baseline"] = None
@@ -333,6 +399,8 @@ def main():
                                "ms_per_step": round(ms_alt, 4), "bytes_in_per_step_all_ranks": alt_bytes}
         if gather_ms is not None:
             out["gather_C_ms"] = round(gather_ms, 3)
+        out["single_gpu_same_matrix"] = one_gpu
+        out["speedup_vs_1gpu"] = round(one_gpu["ms_per_step"] / ms_per_step, 3)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

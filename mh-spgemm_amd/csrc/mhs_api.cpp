@@ -57,6 +57,8 @@ struct mhs_ctx {
     char* slots = nullptr;   // their value slots (cached across calls)
     size_t slots_bytes = 0;
     size_t mem_budget = 0;   // MHS_OPT_MEM_BUDGET (MiB): a call's workspace + C beyond it count as OOM (tests)
+    size_t c_held = 0;       // C bytes a row-chunked call holds while it lays out its second pass
+    long long front_passes = 0;  // front_pass calls (row-chunked passes; mhs_ctx_chunked_calls diagnostics)
     long long chunked_calls = 0;  // calls that ran row-chunked (mhs_ctx_chunked_calls)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays): (buffer, allocation size)
@@ -207,6 +209,10 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     return L;
 }
 
+// Device bytes the context holds for a call: its cached buffers plus C arrays a row-chunked
+// call has already allocated (MHS_OPT_MEM_BUDGET counts them all).
+size_t held(const mhs_ctx* ctx) { return ctx->ws_bytes + ctx->gscratch_bytes + ctx->slots_bytes + ctx->c_held; }
+
 int ensure(mhs_ctx* ctx, char** buf, size_t* have, size_t need) {
     if (*have >= need) return MHS_OK;
     if (*buf) {
@@ -216,8 +222,8 @@ int ensure(mhs_ctx* ctx, char** buf, size_t* have, size_t need) {
         *have = 0;
     }
     size_t want = need + need / 8;
-    if (ctx->mem_budget && want > ctx->mem_budget) want = need;
-    if (ctx->mem_budget && need > ctx->mem_budget)
+    if (ctx->mem_budget && held(ctx) + want > ctx->mem_budget) want = need;
+    if (ctx->mem_budget && held(ctx) + need > ctx->mem_budget)
         return fail(ctx, MHS_ERR_OOM, "workspace exceeds the context's memory budget");
     MHS_HIP(hipMalloc((void**)buf, want));
     *have = want;
@@ -226,7 +232,7 @@ int ensure(mhs_ctx* ctx, char** buf, size_t* have, size_t need) {
 
 // C.col / C.val of nnz entries (+ what the call already holds) within the test budget
 hipError_t alloc_c(mhs_ctx* ctx, mhs_csr* out, long long nnz) {
-    if (ctx->mem_budget && ctx->ws_bytes + (size_t)nnz * 12 > ctx->mem_budget) return hipErrorOutOfMemory;
+    if (ctx->mem_budget && held(ctx) + (size_t)nnz * 12 > ctx->mem_budget) return hipErrorOutOfMemory;
     hipError_t e = pool_get(ctx, (void**)&out->col, (size_t)nnz * 4);
     if (e == hipSuccess) e = pool_get(ctx, (void**)&out->val, (size_t)nnz * 8);
     if (e != hipSuccess) {
@@ -299,6 +305,7 @@ int front_pass(mhs_ctx* ctx, const Csr& a, const Csr& b, Work& w, int* Cptr, boo
     if (rc) return rc;
     memcpy(&h, (const void*)&ctx->pub->stats, sizeof(Stats));
     ctx->stats_zero = true;
+    ++ctx->front_passes;
     return MHS_OK;
 }
 
@@ -330,11 +337,14 @@ void free_cached(mhs_ctx* ctx) {
 }
 
 // Row-chunked product, the fallback when the workspace (or the workspace and C together)
-// does not fit the device: everything cached is given back, the workspace is laid out for
-// Mc rows (halved until it fits), a counting pass over the chunks sizes C, C is allocated
-// once, and a second pass writes every chunk's rows at their offset in C (row_ptr rebased
-// by one small kernel per chunk).  The reference has no such path: Tool::allocate and the
-// C cudaMalloc simply throw (src/Tool.cu:4-45, src/main.cu:54-61).
+// does not fit the device.  Everything cached is given back; a counting pass runs with the
+// largest chunk workspace that fits (Mc rows, halved until it does) and sizes C; the
+// workspace is freed and C allocated -- C's size does not depend on the chunking, so when C
+// alone does not fit the call fails right there, after one pass; then the workspace is laid
+// out again for the memory C leaves (halved only while the workspace itself does not fit)
+// and a second pass writes every chunk's rows at their offset in C (row_ptr rebased by one
+// small kernel per chunk).  The reference has no such path: Tool::allocate and the C
+// cudaMalloc simply throw (src/Tool.cu:4-45, src/main.cu:54-61).
 int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs_timing* t,
                    std::chrono::steady_clock::time_point T0) {
     const int M = A->M, MB = B->M;
@@ -351,60 +361,71 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
         const int est = (int)((long long)A->nnz * (r1 - r0) / (M > 0 ? M : 1));
         return Csr{r1 - r0, A->N, est, A->ptr + r0, A->col, A->val};
     };
-    int nch = 0;
+    // the workspace for chunks of Mc rows (Mc halved from `from` until it fits)
+    auto fit_workspace = [&](int from) {
+        for (Mc = from;;) {
+            if (Mc <= 1) return fail(ctx, MHS_ERR_OOM, "a one-row workspace does not fit the device");
+            Mc = (Mc + 1) / 2;
+            if (ctx->ws) (void)hipFree(ctx->ws);
+            ctx->ws = nullptr;
+            ctx->ws_bytes = 0;
+            ctx->stats_zero = false;
+            mc_list = ctx->mc_list > 0 ? ctx->mc_list : mc_list_for(Mc);
+            L = plan(Mc, MB, A->nnz, B->nnz, mc_list, M);
+            const int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
+            if (rc != MHS_ERR_OOM) return rc;
+            (void)hipGetLastError();
+        }
+    };
+    int rc = fit_workspace(M);
+    if (rc) return rc;
+    // pass 1: counts
+    int nch = (M + Mc - 1) / Mc;
     Stats h{};
     long long total = 0;
     unsigned long long flop = 0;
-    mhs_csr out{};
-    for (;;) {  // halve the chunk until the workspace and then C fit
-        if (Mc <= 1) return fail(ctx, MHS_ERR_OOM, "C and a one-row workspace do not fit the device");
-        Mc = (Mc + 1) / 2;
-        if (ctx->ws) (void)hipFree(ctx->ws);
-        ctx->ws = nullptr;
-        ctx->ws_bytes = 0;
-        ctx->stats_zero = false;
-        mc_list = ctx->mc_list > 0 ? ctx->mc_list : mc_list_for(Mc);
-        L = plan(Mc, MB, A->nnz, B->nnz, mc_list, M);
-        int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
-        if (rc == MHS_ERR_OOM) {
-            (void)hipGetLastError();
-            continue;
-        }
-        if (rc) return rc;
-        // pass 1: counts
-        nch = (M + Mc - 1) / Mc;
+    {
         int* tptr = nullptr;
         MHS_HIP(pool_get(ctx, (void**)&tptr, (size_t)(Mc + 1) * 4));
-        total = 0;
-        flop = 0;
-        for (int c = 0; c < nch; ++c) {
+        for (int c = 0; c < nch && rc == MHS_OK; ++c) {
             const Csr a = view(c);
             Work w = make_work(ctx, L, a.M, a.nnz, B->N, mc_list);
             rc = front_pass(ctx, a, b, w, tptr, c == 0, h);
             if (rc == MHS_OK && h.err)
                 rc = fail(ctx, (h.err & ERR_OVERFLOW) ? MHS_ERR_OVERFLOW : MHS_ERR_INVALID, err_text(h.err));
-            if (rc) {
-                pool_put(ctx, tptr);
-                return rc;
-            }
             total += h.nnzC;
             flop += h.flop;
         }
         pool_put(ctx, tptr);
-        if (total > INT_MAX) return fail(ctx, MHS_ERR_OVERFLOW, "nnz(C) exceeds INT32_MAX");
-        out = mhs_csr{};
-        out.M = M;
-        out.N = B->N;
-        out.nnz = (int)total;
+        if (rc) return rc;
+    }
+    if (total > INT_MAX) return fail(ctx, MHS_ERR_OVERFLOW, "nnz(C) exceeds INT32_MAX");
+    // C before the second pass's workspace: it does not depend on the chunking
+    const int Mc1 = Mc;
+    free_cached(ctx);
+    mhs_csr out{};
+    out.M = M;
+    out.N = B->N;
+    out.nnz = (int)total;
+    {
         hipError_t e = pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4);
         if (e == hipSuccess) e = alloc_c(ctx, &out, total);
-        if (e == hipSuccess) break;
-        pool_put(ctx, out.ptr);
-        (void)hipGetLastError();
-        if (e != hipErrorOutOfMemory) return fail_hip(ctx, e, "allocating C (row-chunked)");
-        for (auto& bf : ctx->pool) (void)hipFree(bf.first);
-        ctx->pool.clear();
+        if (e != hipSuccess) {
+            pool_put(ctx, out.ptr);
+            free_cached(ctx);
+            (void)hipGetLastError();
+            return e == hipErrorOutOfMemory ? fail(ctx, MHS_ERR_OOM, "C itself does not fit the device")
+                                            : fail_hip(ctx, e, "allocating C (row-chunked)");
+        }
     }
+    ctx->c_held = (size_t)(M + 1) * 4 + (size_t)total * 12;
+    rc = fit_workspace(2 * Mc1 - 1);  // (starts at Mc1: the first halving gives it back)
+    ctx->c_held = 0;
+    if (rc) {
+        mhs_csr_free(&out);
+        return rc;
+    }
+    nch = (M + Mc - 1) / Mc;
     // pass 2: every chunk's rows at their offset
     long long off = 0;
     int sym[NBINS] = {}, num[NBINS] = {};
@@ -412,10 +433,11 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
         const Csr a = view(c);
         const int r0 = c * Mc;
         Work w = make_work(ctx, L, a.M, a.nnz, B->N, mc_list);
-        int rc = front_pass(ctx, a, b, w, out.ptr + r0, false, h);
+        rc = front_pass(ctx, a, b, w, out.ptr + r0, c == 0, h);
         if (rc == MHS_OK) rc = ensure_gscratch(ctx, w, h);
         if (rc) {
-            mhs_ctx_recycle(ctx, &out);
+            (void)hipStreamSynchronize(s);
+            mhs_csr_free(&out);
             return rc;
         }
         if (h.nnzC > 0)
@@ -602,7 +624,14 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     if (rc == MHS_ERR_OOM && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
     if (rc) return rc;
     if (ctx->ws != ws_before) ctx->stats_zero = false;
-    MHS_HIP(pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4));
+    {
+        const hipError_t e = pool_get(ctx, (void**)&out.ptr, (size_t)(M + 1) * 4);
+        if (e == hipErrorOutOfMemory && M > 1) {
+            (void)hipGetLastError();
+            return spgemm_chunked(ctx, A, B, C, t, T0);
+        }
+        if (e != hipSuccess) return fail_hip(ctx, e, "allocating C.ptr");
+    }
     Work w = make_work(ctx, L, M, A->nnz, B->N, mc_list);
     // device Stats start zeroed: the previous call's k_scan left them so, else a memset
     if (!ctx->stats_zero) MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
@@ -716,6 +745,8 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     rc = ensure_gscratch(ctx, w, h);
     if (rc) {
         mhs_ctx_recycle(ctx, &out);
+        (void)hipGetLastError();
+        if (rc == MHS_ERR_OOM && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
         return rc;
     }
     const double t_malloc = ms_since(T5);

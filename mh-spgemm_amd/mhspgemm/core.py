@@ -412,6 +412,16 @@ def MH_spgemm(A: CSR, B: CSR, C: CSR, timing: Timing, tools: Tool):
     print(f"C.nnz = {C.nnz}")
 
 
+def _cache_setting(v):
+    """$MHS_MTX_CACHE: unset, "", "0", "false", "no", "off" -> off; "1", "true", "yes", "on" ->
+    next to the file; anything else -> a cache directory."""
+    if v is None or v.strip().lower() in ("", "0", "false", "no", "off"):
+        return False
+    if v.strip().lower() in ("1", "true", "yes", "on"):
+        return True
+    return v
+
+
 def readMtxFile(A: CSR, filename: str, cache=None) -> int:
     """inc/mmio_read.h:34-159 through the library's parallel reader.
 
@@ -420,8 +430,8 @@ def readMtxFile(A: CSR, filename: str, cache=None) -> int:
     mtime instead of the text, writing it on a miss."""
     h = L.mhs_host_csr()
     if cache is None:
-        cache = os.environ.get("MHS_MTX_CACHE") or False
-    if cache and cache is not True and str(cache) not in ("1", "true"):
+        cache = _cache_setting(os.environ.get("MHS_MTX_CACHE"))
+    if cache and cache is not True and str(cache).lower() not in ("1", "true", "yes", "on"):
         d = os.fspath(cache)
         os.makedirs(d, exist_ok=True)
         cpath = os.path.join(d, os.path.basename(str(filename)) + ".mhscsr").encode()

@@ -382,3 +382,45 @@ def load_or_synth(name: str) -> tuple[CSR, str]:
     if name not in SYNTH:
         raise KeyError(f"no synthetic stand-in for {name!r}")
     return _cached(name), f"synthetic:{name}-like"
+
+
+# ---- one host copy for several ranks (bench.py --gpus N) --------------------------
+
+def shared_dir(name: str) -> Path:
+    root = os.environ.get("MHS_SYNTH_CACHE") or f"/tmp/mhs_synth_{os.getuid()}"
+    return Path(root) / f"{name}.csr"
+
+
+def build_shared(name: str) -> str:
+    """Write `name`'s matrix (the file, else the stand-in) as ptr/col/val .npy files
+    under shared_dir(name) unless they exist; returns the source description.  One
+    process per node calls this; the others then `open_shared` (memory-mapped: a rank
+    touches only the pages of its row block)."""
+    d = shared_dir(name)
+    src = d / "source.txt"
+    if src.exists():
+        return src.read_text()
+    A, source = load_or_synth(name)
+    tmp = d.with_name(f"{d.name}.{os.getpid()}.tmp")
+    tmp.mkdir(parents=True, exist_ok=True)
+    np.save(tmp / "ptr.npy", A.ptr)
+    np.save(tmp / "col.npy", A.col)
+    np.save(tmp / "val.npy", A.val)
+    (tmp / "shape.txt").write_text(f"{A.M} {A.N}")
+    (tmp / "source.txt").write_text(source)
+    try:
+        os.replace(tmp, d)
+    except OSError:  # another process got there first
+        import shutil
+        shutil.rmtree(tmp, ignore_errors=True)
+    return (d / "source.txt").read_text()
+
+
+def open_shared(name: str):
+    """(M, N, ptr, col, val, source) of build_shared's files, col/val memory-mapped."""
+    d = shared_dir(name)
+    M, N = (int(x) for x in (d / "shape.txt").read_text().split())
+    ptr = np.load(d / "ptr.npy")
+    col = np.load(d / "col.npy", mmap_mode="r")
+    val = np.load(d / "val.npy", mmap_mode="r")
+    return M, N, ptr, col, val, (d / "source.txt").read_text()

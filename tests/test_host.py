@@ -214,3 +214,21 @@ def test_product_never_imports_oracle():
     pkg = ROOT / "mh-spgemm_amd"
     for f in list(pkg.rglob("*.py")) + list(pkg.rglob("*.cpp")) + list(pkg.rglob("*.hip")) + list(pkg.rglob("*.hpp")):
         assert "oracle" not in f.read_text(errors="ignore").lower().replace("oracle-free", ""), f
+
+
+def test_mtx_cache_env_words(tmp_path, monkeypatch):
+    # MHS_MTX_CACHE=0/false/no/off (any case) means off -- never a directory named
+    # after the word; 1/true/yes/on caches next to the file; anything else is a directory
+    from mhspgemm.core import _cache_setting
+    for off in (None, "", "0", "false", "No", "OFF"):
+        assert _cache_setting(off) is False
+    for on in ("1", "true", "YES", "on"):
+        assert _cache_setting(on) is True
+    assert _cache_setting(str(tmp_path / "c")) == str(tmp_path / "c")
+    f = tmp_path / "m.mtx"
+    f.write_text("%%MatrixMarket matrix coordinate real general\n2 2 2\n1 1 1.0\n2 2 2.0\n")
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("MHS_MTX_CACHE", "false")
+    A = mhspgemm.CSR()
+    assert mhspgemm.readMtxFile(A, str(f)) == 0 and A.nnz == 2
+    assert not (tmp_path / "false").exists() and not (tmp_path / "m.mtx.mhscsr").exists()
