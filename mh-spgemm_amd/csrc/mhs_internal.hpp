@@ -54,47 +54,20 @@ constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so a numeric tiny row spans
 // 8-lane teams -- eight rows per wave, so one dependent load chain (row -> A -> bmeta -> B)
 // serves eight rows: (8,1) (8,4) (8,8) (32,4).  Numeric keeps its values beside the keys
 // and sums segments per slot, so wide slots cost more: (4,2) (8,4) (16,4) (32,4) (64,4) (64,8).
-// MHS_TINY_SET=0: round 1's classes (8,1) (32,1) (32,2) (32,4) (64,4) (64,8) for both.
-#ifndef MHS_TINY_SET
-#define MHS_TINY_SET 1
-#endif
-#ifndef MHS_TINY0_W4
-#define MHS_TINY0_W4 1  // numeric class 0 as (4,2): 16 rows of <= 4 A entries per wave (GAP-road-like -8 %)
-#endif
-#ifndef MHS_TINY2_W16
-#define MHS_TINY2_W16 1  // numeric class 2 as (16,4) instead of (32,2) (delaunay-like -12 %, mac_econ-like numeric -9 %)
-#endif
-#ifndef MHS_TINY1_W4
-#define MHS_TINY1_W4 0  // numeric class 1 as (4,8) instead of (8,4)
-#endif
-#ifndef MHS_TINYS0_W4
-#define MHS_TINYS0_W4 0  // the same for symbolic class 0
-#endif
-#if MHS_TINY_SET
-__host__ __device__ constexpr int tiny_w(int c) {
-    return c == 0 && MHS_TINY0_W4 ? 4 : c == 1 && MHS_TINY1_W4 ? 4 : c == 2 && MHS_TINY2_W16 ? 16 : c <= 1 ? 8 : c <= 3 ? 32 : 64;
-}
-__host__ __device__ constexpr int tiny_k(int c) {
-    return c == 0 ? (MHS_TINY0_W4 ? 2 : 1) : c == 1 ? (MHS_TINY1_W4 ? 8 : 4) : c == 2 ? (MHS_TINY2_W16 ? 4 : 2) : c == 5 ? 8 : 4;
-}
-__host__ __device__ constexpr int tiny_ws(int c) { return c == 0 && MHS_TINYS0_W4 ? 4 : c <= 2 ? 8 : 32; }
-__host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? (MHS_TINYS0_W4 ? 2 : 1) : c == 2 ? 8 : 4; }
-#else
-__host__ __device__ constexpr int tiny_w(int c) { return c == 0 ? 8 : c <= 3 ? 32 : 64; }
-__host__ __device__ constexpr int tiny_k(int c) { return c <= 1 ? 1 : c == 2 ? 2 : c <= 4 ? 4 : 8; }
-__host__ __device__ constexpr int tiny_ws(int c) { return tiny_w(c); }
-__host__ __device__ constexpr int tiny_ks(int c) { return tiny_k(c); }
-#endif
-constexpr int TINY_FUSED_KMAX = MHS_TINY1_W4 ? 8 : 4;  // largest K of the numeric classes 0..3 (one fused launch)
+// Measured per class: numeric class 0 as (4,2) (GAP-road-like -8 %), class 2 as
+// (16,4) instead of (32,2) (delaunay-like -12 %); (4,8) for class 1 and (4,2) for symbolic
+// class 0 were slower or neutral.
+__host__ __device__ constexpr int tiny_w(int c) { return 4 << (c < 4 ? c : 4); }  // 4 8 16 32 64 64
+__host__ __device__ constexpr int tiny_k(int c) { return c == 0 ? 2 : c == 5 ? 8 : 4; }
+__host__ __device__ constexpr int tiny_ws(int c) { return c <= 2 ? 8 : 32; }
+__host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? 1 : c == 2 ? 8 : 4; }
+constexpr int TINY_FUSED_KMAX = 4;  // largest K of the numeric classes 0..3 (one fused launch)
 // Symbolic uses the classes below TINY_SYM_NC only (past 128 products a hash table
 // counts faster than a sort); numeric uses the 64-lane classes for rows whose table
 // would not fit the small wave bin (measured: cop20k-like 2.3x slower sorted, while
 // rows that need big tables run 2x faster sorted).
 constexpr int TINY_SYM_NC = 4;
-#ifndef MHS_TINY_NUM_SMALL
-#define MHS_TINY_NUM_SMALL 4
-#endif
-constexpr int TINY_NUM_SMALL = MHS_TINY_NUM_SMALL;  // numeric classes >= this only replace big-table rows
+constexpr int TINY_NUM_SMALL = 4;  // numeric classes >= this only replace big-table rows
 __host__ __device__ inline int tiny_class(int flop, int nA, int nc = TINY_NC) {
     if (flop <= 0) return -1;
     for (int c = 0; c < nc; ++c)
@@ -135,17 +108,11 @@ constexpr int SYM_WAVE_WORK = 4096;     // tile products a single wave takes on
 constexpr int SYM_WM_BYTES = (LDS_MAX_C - 1024) / 16;  // 16 waves of a 1024-thread block (k_sym_rare): 16 waves per CU
 constexpr int SYM_B256_BYTES = 32768;
 constexpr int SYM_B256_WORK = 1 << 20;
-#ifndef MHS_NUM_WS_BYTES
-#define MHS_NUM_WS_BYTES 5120
-#endif
-constexpr int NUM_WS_BYTES = MHS_NUM_WS_BYTES;   // 4 waves x 5 KiB = 20 KiB/block: 8 blocks (32 waves) per CU
+constexpr int NUM_WS_BYTES = 5120;     // 4 waves x 5 KiB = 20 KiB/block: 8 blocks (32 waves) per CU
 constexpr int NUM_WS_WORK = 8192;       // products a single wave takes on
 constexpr int NUM_W16_BYTES = 16384;
 constexpr int NUM_W16_WORK = 32768;
-#ifndef MHS_NUM_WSG_BYTES
-#define MHS_NUM_WSG_BYTES 10240
-#endif
-constexpr int NUM_WSG_BYTES = MHS_NUM_WSG_BYTES;  // grouped rows: 4 waves x 10 KiB = 40 KiB/block (4 per CU)
+constexpr int NUM_WSG_BYTES = 10240;   // grouped rows: 4 waves x 10 KiB = 40 KiB/block (4 per CU)
 constexpr int NUM_B256_BYTES = 65536;
 constexpr int NUM_B256_WORK = 1 << 22;
 constexpr int LDS_MAX = 163840;         // gfx950: 160 KiB per workgroup (probed on the box)
@@ -237,12 +204,10 @@ __host__ __device__ inline long long sym_need(int span, int tflop) {
 //             (n doubles): a product lands at base(tile) + popc(mask & below(col));
 //   NM_HASH   scattered rows: hashed tile table + rank-compressed accumulator
 //             (tiles sorted by key to assign bases).
-enum NumMode : int { NM_DENSE = 0, NM_DIRECT = 1, NM_HASH = 2, NM_RMAP = 3 };
+// (A column -> rank map over the span, a uint16 per column, measured 25 % slower than
+// NM_DIRECT on cant-like: dropped.)
+enum NumMode : int { NM_DENSE = 0, NM_DIRECT = 1, NM_HASH = 2 };
 constexpr int MCACHE_SPAN = 32;   // rows spanning <= 32 tiles: symbolic keeps their tile masks
-#ifndef MHS_RMAP_SPAN
-#define MHS_RMAP_SPAN 0  // rank map off: measured 25% slower than DIRECT on cant-like
-#endif
-constexpr int RMAP_SPAN_MAX = MHS_RMAP_SPAN; // NM_RMAP: column -> rank map (uint16 per column of the span)
 __host__ __device__ inline long long num_need_dense(int span) { return (long long)span * (16 + 64 * 8); }
 __host__ __device__ inline long long num_need_direct(int span, int n) {
     return (long long)span * 16 + align16((long long)n * 8);
@@ -256,9 +221,6 @@ __host__ __device__ inline long long num_need_hash(int t, int n) {
     const int h = hash_slots(t);
     const int p = hash_sort_p(t);
     return (long long)h * 16 + align16((long long)(n > p ? n : p) * 8);
-}
-__host__ __device__ inline long long num_need_rmap(int span, int n) {
-    return (long long)span * 16 + align16((long long)span * 64 * 2) + align16((long long)n * 8);
 }
 // symbolic stores the OR'd tile masks of rows it tabled direct-mapped over a narrow span
 __host__ __device__ inline bool mcached(int span, int tflop) { return span <= MCACHE_SPAN && sym_direct(span, tflop); }
@@ -282,7 +244,6 @@ __host__ __device__ inline bool mlisted(int span, int tflop, int t, int list) {
 }
 __host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_max) {
     if (span <= dense_span_max) return NM_DENSE;
-    if (span <= RMAP_SPAN_MAX) return NM_RMAP;
     // direct-mapped (no probes, no tile sort) unless it needs more LDS than a hash table
     // at load 1/2 would: the tighter hash sizing only shrinks the rows that hash anyway
     const long long hash_half = (long long)next_pow2(2 * (t < 1 ? 1 : t)) * 16 +
@@ -295,12 +256,9 @@ __host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_m
 __host__ __device__ inline bool num_wide(int span, int t, int n, int dense_span_max);
 __host__ __device__ inline long long num_need(int span, int t, int n, int dense_span_max) {
     const int m = num_mode(span, t, n, dense_span_max);
-    return m == NM_DENSE ? num_need_dense(span) : m == NM_RMAP ? num_need_rmap(span, n)
-                                               : m == NM_DIRECT ? num_need_direct(span, n) : num_need_hash(t, n);
+    return m == NM_DENSE ? num_need_dense(span) : m == NM_DIRECT ? num_need_direct(span, n) : num_need_hash(t, n);
 }
-#ifndef MHS_SPANRANK
-#define MHS_SPANRANK 1  // hub rows past the 256-thread hash budget: rank tiles by a span bitmap
-#endif
+// Hub rows past the 256-thread hash budget rank their tiles by a span bitmap.
 // Span-bitmap rows (num_row_bitmap): span/64 * 12 bytes + 16 per tile + 8 per C entry.
 __host__ __device__ inline long long num_need_ranked(int span, int t, int n) {
     const long long nw = ((long long)span + 63) >> 6;
@@ -310,7 +268,7 @@ __host__ __device__ inline bool num_big_hash(int span, int t, int n, int dense_s
     return num_mode(span, t, n, dense_span_max) == NM_HASH && num_need_hash(t, n) > NUM_B256_BYTES - BLOCK_HDR;
 }
 __host__ __device__ inline bool num_ranked(int span, int t, int n, int dense_span_max) {
-    return MHS_SPANRANK && num_big_hash(span, t, n, dense_span_max) && num_need_ranked(span, t, n) <= B1024_BYTES;
+    return num_big_hash(span, t, n, dense_span_max) && num_need_ranked(span, t, n) <= B1024_BYTES;
 }
 __host__ __device__ inline bool num_wide(int span, int t, int n, int dense_span_max) {
     return num_big_hash(span, t, n, dense_span_max) && !num_ranked(span, t, n, dense_span_max);

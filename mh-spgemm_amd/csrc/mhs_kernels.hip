@@ -30,11 +30,8 @@
 #include <algorithm>
 #include <climits>
 
-#ifndef MHS_NUM_DIAG
-#define MHS_NUM_DIAG 0  // != 0 only in tools/diag timing builds (wrong results by design)
-#endif
-#ifndef MHS_SAMEPAT
-#define MHS_SAMEPAT 1  // detect runs of same-pattern B rows (FEM dof blocks)
+#ifndef MHS_ROW_STAMPS
+#define MHS_ROW_STAMPS 0  // 1: tools/diag/stamps*.py builds -- per-row, per-phase s_memtime cycles
 #endif
 #ifndef MHS_RUN_MAX
 #define MHS_RUN_MAX 3  // longest run a value walk merges into one accumulate (1..4)
@@ -84,15 +81,6 @@
 #ifndef MHS_GRP_UNROLL
 #define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
 #endif
-#ifndef MHS_PIPE
-#define MHS_PIPE 0  // software-pipelined value walk
-#endif
-#ifndef MHS_NUM_WAVES_EU
-#define MHS_NUM_WAVES_EU 1  // occupancy floor the wave numeric kernel is compiled for
-#endif
-#ifndef MHS_BLOCKDIST
-#define MHS_BLOCKDIST 1  // A entries -> lane groups: 1 block distribution, 0 cyclic
-#endif
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice).  The wave kernels are
 // bound by per-row latency chains, so waves in flight matter more than a few spills.
 #ifndef MHS_WPE_HASH
@@ -114,7 +102,7 @@
 #ifndef MHS_WPE_SYM
 #define MHS_WPE_SYM 8  // symbolic wave + tiny kernels: cant-like -12%, cop20k-like -22%
 #endif
-#if MHS_NUM_DIAG == 9  // diagnostic build: per-row, per-phase s_memtime cycles (plain stores)
+#if MHS_ROW_STAMPS  // diagnostic build: per-row, per-phase s_memtime cycles (plain stores)
 __device__ unsigned long long* g_rowdiag;  // [M][8]
 #define MHS_STAMP0() unsigned long long tp_ = __builtin_amdgcn_s_memtime()
 #define MHS_STAMP(k)                                                    \
@@ -212,76 +200,30 @@ __device__ __forceinline__ int hnext(int s, int H) { return s + 1 < H ? s + 1 : 
 __device__ __forceinline__ int sat_int(long long x) { return x > INT_MAX ? INT_MAX : (int)x; }
 __device__ __forceinline__ int hi_lo_span(int lo, int hi) { return hi - lo + 1; }
 
-// Streaming accesses (C, the symbolic -> numeric row cache): each byte is written or read
-// once, so they bypass L2 allocation (nontemporal) and leave the XCD's 4 MiB to the B rows
-// that neighbouring C rows share.
-#ifndef MHS_NT
-#define MHS_NT 1
-#endif
-#ifndef MHS_NT_PART
-#define MHS_NT_PART 0
-#endif
-// Write-once stores can also DROP their line from the XCD's L2 (gfx950: an agent-scope
-// relaxed atomic store is a plain `global_store ... sc1`; `nt` and plain stores keep the
-// line).  Measured (r03_sc1, 8 stand-ins, two interleaved rounds): C stores dropped made
-// cant-like numeric +6 %, cage15-like +4 %, cage12-like +11 %; wb-edu-like within noise;
-// the row cache and partial-line stores dropped too: worse again.  Knobs off.
-#ifndef MHS_SC1_C
-#define MHS_SC1_C 0
-#endif
-#ifndef MHS_SC1_PART
-#define MHS_SC1_PART 0
-#endif
-#ifndef MHS_SC1_MC
-#define MHS_SC1_MC 0
-#endif
-template <class T>
-__device__ __forceinline__ void st_drop(T* p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// Streaming stores (C): each byte is written once, so they bypass L2 allocation
+// (nontemporal) and leave the XCD's 4 MiB to the B rows that neighbouring C rows share.
+// Measured and dropped: stores that drop their line from L2 (`sc1`), and
+// nontemporal row-cache / partial-line traffic.
 template <class T>
 __device__ __forceinline__ void st_stream(T* p, T v) {
-#if MHS_SC1_C
-    st_drop(p, v);
-#elif MHS_NT
     __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
 }
 // Stores that leave partial cache lines (a tile's set bits, a tiny row's segment ends) stay
 // cached: L2 merges them into whole lines; nontemporal they reach HBM as masked partial
 // writes (measured: WRITE_SIZE 1.32x C's bytes on cant-like).
 template <class T>
 __device__ __forceinline__ void st_part(T* p, T v) {
-#if MHS_SC1_PART
-    st_drop(p, v);
-#elif MHS_NT_PART
-    __builtin_nontemporal_store(v, p);
-#else
     *p = v;
-#endif
 }
-#ifndef MHS_NT_MC
-#define MHS_NT_MC 0  // the row cache too (measured: cage15-like symbolic +3.5%, cop20k-like numeric +4%)
-#endif
+// The symbolic -> numeric row cache: plain (cached) stores and loads (measured: nontemporal
+// made cage15-like symbolic +3.5 %, cop20k-like numeric +4 %)
 template <class T>
 __device__ __forceinline__ void st_cache(T* p, T v) {
-#if MHS_SC1_MC
-    st_drop(p, v);
-#elif MHS_NT_MC
-    __builtin_nontemporal_store(v, p);
-#else
     *p = v;
-#endif
 }
 template <class T>
 __device__ __forceinline__ T ld_cache(const T* p) {
-#if MHS_NT_MC
-    return __builtin_nontemporal_load(p);
-#else
     return *p;
-#endif
 }
 
 // Lane-group width for walking the products of one row: groups of G lanes
@@ -289,15 +231,12 @@ __device__ __forceinline__ T ld_cache(const T* p) {
 // ceil(nA / groups) * ceil(avg B-row length / G) (ties -> wider, better
 // coalesced groups); at most 64 groups so one staged chunk of 64 A entries
 // feeds every group.
-#ifndef MHS_PICK_U
-#define MHS_PICK_U 1  // count load batches of U entries per lane in the sweep cost (0: entries)
-#endif
 __device__ __forceinline__ int pick_group(long long work, int nA, int T, int gfloor = 4, int unroll = 1) {
     int gmin = T / 64;
     if (gmin < gfloor) gmin = gfloor;
     if (nA <= 0) return gmin;
     const long long avg = (work + nA - 1) / nA;
-    const int U = MHS_PICK_U ? unroll : 1;
+    const int U = unroll;
     int best = gmin;
     long long bc = LLONG_MAX;
     for (int g = gmin; g <= T; g <<= 1) {
@@ -349,7 +288,7 @@ __device__ __forceinline__ StagedChunk stage_chunk(int lane, int jb, int a1,
         const int4 m = bmeta[k];
         x.st = m.x;
         x.ln = tiles ? meta_ntiles(m) : m.y;
-        cont = MHS_SAMEPAT && lane > 0 && meta_same(m) && kp == k - 1;
+        cont = lane > 0 && meta_same(m) && kp == k - 1;
         if (Aval) x.av = Aval[jl];
     }
     const unsigned long long C = __ballot(cont);
@@ -404,19 +343,6 @@ struct RowWalk {
     }
 };
 
-#ifndef MHS_SPILL
-#define MHS_SPILL 1  // symbolic keeps the tile lists of rows past the row-cache cap for numeric
-#endif
-#ifndef MHS_WAVE_CHUNKS
-#define MHS_WAVE_CHUNKS 0  // > 0: block teams walk rows of >= this many A entries per thread wave-by-wave
-                           // (measured: webbase-like numeric +10%, wb-edu-like symbolic -8%: off)
-#endif
-#ifndef MHS_DYN
-#define MHS_DYN 0  // > 0: wave bins take MHS_DYN consecutive list entries at a time from a cursor
-#endif
-#ifndef MHS_GUIDED16
-#define MHS_GUIDED16 1  // guided walk (see num_wave_rows) in the numeric 16 KiB bins: 1 hash, 2 direct/grouped
-#endif
 #ifndef MHS_GRP_CHUNK
 #define MHS_GRP_CHUNK 63  // A entries staged per chunk in the grouped walk (<= 64)
 #endif
@@ -459,19 +385,12 @@ struct WaveQueue {
     }
 };
 
-#ifndef MHS_BLKQ
-#define MHS_BLKQ 1  // block-per-row walks (k_sym_rare, k_num_block) take rows from one global cursor
-#endif
-#ifndef MHS_BLKQ_NUM
-#define MHS_BLKQ_NUM MHS_BLKQ
-#endif
-#ifndef MHS_BLKQ_SYMB
-#define MHS_BLKQ_SYMB 0  // k_sym_block<256> too: measured cant-s1-like symbolic +12 %, scircuit-like +12 %
-#endif              // (tens of thousands of uniform rows: one cursor contended, the static walk balanced)
-// Dynamic row queue of a block team: thread 0 takes the next list index from the launch's
-// cursor (one atomic per row: the block bins hold hundreds to a few thousand rows), the
-// block reads it between two barriers.  Power-law rows differ by orders of magnitude in
-// cost; a static stride left the kernel's end to the block that drew the heaviest rows.
+// Dynamic row queue of a block team (k_sym_rare, k_num_block): thread 0 takes the next list
+// index from the launch's cursor (one atomic per row: the block bins hold hundreds to a few
+// thousand rows), the block reads it between two barriers.  Power-law rows differ by orders
+// of magnitude in cost; a static stride left the kernel's end to the block that drew the
+// heaviest rows.  (k_sym_block<256> keeps its static walk: tens of thousands of uniform rows
+// on one cursor measured +12 % on cant-s1- and scircuit-like.)
 struct BlockQueue {
     int* cur;
     int* slot;  // an LDS word
@@ -593,26 +512,21 @@ __device__ void team_bitonic(const Team& tm, unsigned long long* S, int P) {
 // DPP quad_perm for d = 1, 2; DPP row shifts + select for d = 4, 8 (both neighbours are
 // inside the lane's 16-lane row); ds_swizzle (xor mode, no LDS memory access) for 16;
 // ds_bpermute only for 32.  Every lane of the wave must be active.
-#ifndef MHS_DPP
-#define MHS_DPP 1
-#endif
 __device__ __forceinline__ int xor_lanes(int v, int d) {
-    if (MHS_DPP) {
-        const int lane = lane_id();
-        if (d == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-        if (d == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-        if (d == 4) {
-            const int up = __builtin_amdgcn_mov_dpp(v, 0x104, 0xF, 0xF, false);  // row_shl:4  (lane + 4)
-            const int dn = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4  (lane - 4)
-            return (lane & 4) ? dn : up;
-        }
-        if (d == 8) {
-            const int up = __builtin_amdgcn_mov_dpp(v, 0x108, 0xF, 0xF, false);  // row_shl:8
-            const int dn = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
-            return (lane & 8) ? dn : up;
-        }
-        if (d == 16) return __builtin_amdgcn_ds_swizzle(v, 0x401F);  // and 0x1F, xor 0x10
+    const int lane = lane_id();
+    if (d == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    if (d == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    if (d == 4) {
+        const int up = __builtin_amdgcn_mov_dpp(v, 0x104, 0xF, 0xF, false);  // row_shl:4  (lane + 4)
+        const int dn = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4  (lane - 4)
+        return (lane & 4) ? dn : up;
     }
+    if (d == 8) {
+        const int up = __builtin_amdgcn_mov_dpp(v, 0x108, 0xF, 0xF, false);  // row_shl:8
+        const int dn = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
+        return (lane & 8) ? dn : up;
+    }
+    if (d == 16) return __builtin_amdgcn_ds_swizzle(v, 0x401F);  // and 0x1F, xor 0x10
     return __shfl_xor(v, d);
 }
 
@@ -637,14 +551,6 @@ __device__ __forceinline__ int row_bcast31(int v) {  // lane 31 -> rows 2, 3 (in
 // Inclusive scan over teams of W lanes (aligned groups of W consecutive lanes).
 template <int W>
 __device__ __forceinline__ int team_incl_scan(int x, int tl) {
-    if (!MHS_DPP) {
-#pragma unroll
-        for (int d = 1; d < W; d <<= 1) {
-            const int o = __shfl_up(x, d, W);
-            x += tl >= d ? o : 0;
-        }
-        return x;
-    }
 #pragma unroll
     for (int d = 1; d < (W < 16 ? W : 16); d <<= 1) {
         const int o = row_shr(x, d);
@@ -658,17 +564,6 @@ __device__ __forceinline__ int team_incl_scan(int x, int tl) {
 // Segmented inclusive sum over teams of W lanes: a lane with `seen` set starts a segment.
 template <int W>
 __device__ __forceinline__ double team_seg_scan(double sum, bool seen, int tl) {
-    if (!MHS_DPP) {
-#pragma unroll
-        for (int d = 1; d < W; d <<= 1) {
-            const double os = __shfl_up(sum, d, W);
-            const int of = __shfl_up((int)seen, d, W);
-            const bool add = tl >= d && !seen;
-            sum += add ? os : 0.0;
-            seen = add ? of != 0 : seen;
-        }
-        return sum;
-    }
 #pragma unroll
     for (int d = 1; d < (W < 16 ? W : 16); d <<= 1) {
         const int oh = row_shr(__double2hiint(sum), d), ol = row_shr(__double2loint(sum), d);
@@ -1086,46 +981,6 @@ __device__ __forceinline__ void run_segment_run(const F& f, int s, int n, int gl
     int o[LM];
 #pragma unroll
     for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
-#if MHS_PIPE
-    // software pipeline: batch t+1's loads are in flight while batch t accumulates
-    // (indices past the segment are clamped to its first entry and not accumulated)
-    if (gl >= n) return;
-    int c0[U], c1[U];
-    double b0[U][LM], b1[U][LM];
-    auto ld = [&](int q, int (&c)[U], double (&b)[U][LM]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int qq = q + u * G < n ? q + u * G : gl;
-            c[u] = f.col(s + qq);
-#pragma unroll
-            for (int i = 0; i < LM; ++i) b[u][i] = f.val(s + o[i] + qq);
-#pragma unroll
-            for (int i = 1; i < LM; ++i) pin(b[u][i]);
-        }
-    };
-    ld(gl, c0, b0);
-    for (int q = gl;; q += U * G) {
-        const bool more = q + U * G < n;
-        ld(more ? q + U * G : gl, c1, b1);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (q + u * G < n) {
-                double v = a[0] * b0[u][0];
-#pragma unroll
-                for (int i = 1; i < LM; ++i) v += i < L ? a[i] * b0[u][i] : 0.0;
-                f.add(c0[u], v);
-            }
-        }
-        if (!more) break;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            c0[u] = c1[u];
-#pragma unroll
-            for (int i = 0; i < LM; ++i) b0[u][i] = b1[u][i];
-        }
-    }
-    return;
-#endif
     // U entries per lane per batch, a short segment's tail included: indices past the
     // segment are clamped to the batch's first entry (a cache hit, not accumulated), so
     // a segment of <= U*G entries costs one load round trip, not one per entry
@@ -1220,7 +1075,7 @@ __device__ __forceinline__ void wave_chunks(int jb0, int jstep, int a1, const in
             // block distribution: groups run A entries far apart in the row at the same
             // time (neighbouring entries share B columns and would collide on the same
             // accumulator words)
-            const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
+            const int e = grp * iters + it;
             const int h = __shfl(x.src, e & 63);  // all lanes active at the shuffles
             const int s = __shfl(x.st, h);
             const int n0 = __shfl(x.ln, h);
@@ -1285,7 +1140,7 @@ __device__ __forceinline__ void for_products_group(int a0, int a1, const int* __
         const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
         const int iters = (x.nh + ngrp - 1) / ngrp;
         for (int it = 0; it < iters; ++it) {
-            const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
+            const int e = grp * iters + it;
             const int h = __shfl(x.src, e & 63);
             const int sb = __shfl(x.st, h);
             const int n0 = __shfl(x.ln, h);
@@ -1403,7 +1258,7 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
             const int grp = threadIdx.x >> gs, gl = threadIdx.x & (G - 1), ngrp = T >> gs;  // ngrp <= 64
             const int iters = (nloc + ngrp - 1) / ngrp;
             for (int it = 0; it < iters; ++it) {
-                const int e = MHS_BLOCKDIST ? grp * iters + it : it * ngrp + grp;
+                const int e = grp * iters + it;
                 if (e >= nloc) continue;
                 const int4 v = sg[1 + e];
                 if constexpr (F::kValues) {
@@ -1430,133 +1285,9 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
     }
 }
 
-// Flattened walk (long B segments): the products of the chunk's A entries are
-// laid end to end; a batch is 64 consecutive products, one per lane, so one
-// load instruction touches at most a couple of B rows (coalesced, every lane
-// busy).  The A entries overlapping a batch are found with a short uniform
-// loop over the chunk's inclusive prefix of segment lengths (readlane on a
-// wave, broadcast LDS reads on a block); U batches issue their loads together.
-template <class F>
-__device__ __forceinline__ void for_products_flat(const WaveTeam&, int a0, int a1,
-                                                  const int* __restrict__ Acol,
-                                                  const double* __restrict__ Aval,
-                                                  const int4* __restrict__ bmeta, bool tiles,
-                                                  const F& f, int4*) {
-    constexpr int U = 2;
-    const int lane = lane_id();
-    for (int jb = a0; jb < a1; jb += 64) {
-        const int jl = jb + lane;
-        int st = 0, ln = 0;
-        double av = 0.0;
-        if (jl < a1) {
-            const int k = Acol[jl];
-            const int4 m = bmeta[k];
-            st = m.x;
-            ln = tiles ? meta_ntiles(m) : m.y;
-            if (Aval) av = Aval[jl];
-        }
-        const int nloc = min(64, a1 - jb);
-        const int incl = wave_incl_scan(ln);
-        const int excl = incl - ln;
-        const int avlo = __double2loint(av), avhi = __double2hiint(av);
-        const int total = __builtin_amdgcn_readlane(incl, 63);
-        int jj = 0;  // first entry whose range ends after the current batch start
-        for (int P0 = 0; P0 < total; P0 += 64 * U) {
-            int idx[U];
-            double aa[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int B0 = P0 + 64 * u;
-                const int p = B0 + lane;
-                idx[u] = -1;
-                aa[u] = 0.0;
-                while (jj < nloc && __builtin_amdgcn_readlane(incl, jj) <= B0) ++jj;
-                for (int j2 = jj; j2 < nloc; ++j2) {
-                    const int s = __builtin_amdgcn_readlane(excl, j2);
-                    if (s >= B0 + 64) break;
-                    const int e = __builtin_amdgcn_readlane(incl, j2);
-                    if (p >= s && p < e) {
-                        idx[u] = __builtin_amdgcn_readlane(st, j2) + (p - s);
-                        aa[u] = __hiloint2double(__builtin_amdgcn_readlane(avhi, j2),
-                                                 __builtin_amdgcn_readlane(avlo, j2));
-                    }
-                }
-            }
-            // loads unconditional (clamped index): a branch around each load would
-            // make hipcc wait vmcnt(0) per element and serialise the batch
-            typename F::Item x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = f.load(idx[u] >= 0 ? idx[u] : 0);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (idx[u] >= 0) f.put(x[u], aa[u]);
-        }
-    }
-}
-
-template <int T, bool GM, class F>
-__device__ __forceinline__ void for_products_flat(const BlockTeam<T, GM>&, int a0, int a1,
-                                                  const int* __restrict__ Acol,
-                                                  const double* __restrict__ Aval,
-                                                  const int4* __restrict__ bmeta, bool tiles,
-                                                  const F& f, int4* stage) {
-    constexpr int U = 2;
-    constexpr int W = T / 64;
-    const int lane = lane_id(), wv = threadIdx.x >> 6;
-    for (int jb = a0; jb < a1; jb += 64) {
-        if (threadIdx.x < 64) {  // wave 0 stages the chunk: {start, incl prefix, a lo, a hi}
-            const int jl = jb + lane;
-            int st = 0, ln = 0;
-            double av = 0.0;
-            if (jl < a1) {
-                const int k = Acol[jl];
-                const int4 m = bmeta[k];
-                st = m.x;
-                ln = tiles ? meta_ntiles(m) : m.y;
-                if (Aval) av = Aval[jl];
-            }
-            const int incl = wave_incl_scan(ln);
-            stage[lane] = make_int4(st, incl, __double2loint(av), __double2hiint(av));
-        }
-        __syncthreads();
-        const int nloc = min(64, a1 - jb);
-        const int total = stage[63].y;
-        int jj = 0;
-        for (int P0 = 64 * U * wv; P0 < total; P0 += 64 * U * W) {
-            int idx[U];
-            double aa[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int B0 = P0 + 64 * u;
-                const int p = B0 + lane;
-                idx[u] = -1;
-                aa[u] = 0.0;
-                while (jj < nloc && stage[jj].y <= B0) ++jj;
-                for (int j2 = jj; j2 < nloc; ++j2) {
-                    const int4 v = stage[j2];
-                    const int s = j2 ? stage[j2 - 1].y : 0;
-                    if (s >= B0 + 64) break;
-                    if (p >= s && p < v.y) {
-                        idx[u] = v.x + (p - s);
-                        aa[u] = __hiloint2double(v.w, v.z);
-                    }
-                }
-            }
-            // loads unconditional (clamped index): a branch around each load would
-            // make hipcc wait vmcnt(0) per element and serialise the batch
-            typename F::Item x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = f.load(idx[u] >= 0 ? idx[u] : 0);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (idx[u] >= 0) f.put(x[u], aa[u]);
-        }
-        __syncthreads();
-    }
-}
-
-// Lane groups (the flattened walk is kept as an experiment: its per-batch
-// owner search costs more instructions than it saves in coalescing).
+// Lane groups (a flattened walk -- 64 consecutive products per batch, the owner of each
+// found by a search over the chunk's prefix of segment lengths -- measured slower: its
+// per-batch owner search costs more instructions than it saves in coalescing).
 template <class Team, class F>
 __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
                                               const int* __restrict__ Acol,
@@ -1564,20 +1295,10 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
                                               const int4* __restrict__ bmeta, bool tiles,
                                               long long work, const F& f, int4* stage) {
     const int nA = a1 - a0;
-    if (MHS_NUM_DIAG == 6 && nA > 0 && work >= 8LL * nA)  // flattened walk: experiment only (slower)
-        for_products_flat(tm, a0, a1, Acol, Aval, bmeta, tiles, f, stage);
-    else if (Team::size > 64 && MHS_WAVE_CHUNKS > 0 && nA >= MHS_WAVE_CHUNKS * Team::size)
-        // long A rows (hubs of power-law matrices: thousands of entries on short B rows): every
-        // wave walks its own 64-entry chunks wv, wv + W, ... of the row -- no stage, no barrier
-        // (a staged round chains A entry -> bmeta -> B load round trips behind two barriers
-        // per 64*STAGE_SUBS entries)
-        wave_chunks(a0 + 64 * (tm.rank() >> 6), Team::size, a1, Acol, Aval, bmeta, tiles,
-                    pick_group(work, nA, 64, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN, tiles ? 1 : MHS_UNROLL), f);
-    else
-        for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
-                     pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN,
-                                tiles ? 1 : (Team::size > 64 ? MHS_UNROLL_BLOCK : MHS_UNROLL)),  // (tile walks: by entries)
-                     f, stage);
+    for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
+                 pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN,
+                            tiles ? 1 : (Team::size > 64 ? MHS_UNROLL_BLOCK : MHS_UNROLL)),  // (tile walks: by entries)
+                 f, stage);
 }
 
 // ---------------------------------------------------------- tile tables ---
@@ -1624,7 +1345,6 @@ struct Accum {
     static constexpr bool kValues = true;
     const TileEntry* E;
     double* acc;
-    const unsigned short* rmap;
     int lo, H, colbase;
     const int* __restrict__ Bcol;
     const double* __restrict__ Bval;
@@ -1632,41 +1352,12 @@ struct Accum {
         int c;
         double v;
     };
-    __device__ __forceinline__ Item load(int i) const {
-#if MHS_NUM_DIAG == 4  // diagnostic build: no B loads
-        return Item{colbase + (i & 63), (double)i};
-#else
-        return Item{Bcol[i], Bval[i]};
-#endif
-    }
-    __device__ __forceinline__ int col(int i) const {
-#if MHS_NUM_DIAG == 4
-        return colbase + (i & 63);
-#else
-        return Bcol[i];
-#endif
-    }
-    __device__ __forceinline__ double val(int i) const {
-#if MHS_NUM_DIAG == 4
-        return (double)i;
-#else
-        return Bval[i];
-#endif
-    }
+    __device__ __forceinline__ Item load(int i) const { return Item{Bcol[i], Bval[i]}; }
+    __device__ __forceinline__ int col(int i) const { return Bcol[i]; }
+    __device__ __forceinline__ double val(int i) const { return Bval[i]; }
     __device__ __forceinline__ void put(const Item& x, double a) const { add(x.c, a * x.v); }
     // acc[column c] += v
-    __device__ __forceinline__ void add(int c, double v) const {
-#if MHS_NUM_DIAG == 3  // diagnostic build: no LDS work at all
-        asm volatile("" ::"v"(c), "v"(v));
-        return;
-#endif
-        const int idx = index(c);
-#if MHS_NUM_DIAG == 1  // diagnostic build: plain LDS store instead of the atomic add
-        acc[idx] = v;
-#else
-        acc_add<GM>(&acc[idx], v);
-#endif
-    }
+    __device__ __forceinline__ void add(int c, double v) const { acc_add<GM>(&acc[index(c)], v); }
     // row group: accumulator slice r (stride `stride` doubles) of column c += v[r], r < R
     template <int RM>
     __device__ __forceinline__ void add_rows(int c, const double (&v)[RM], int R, int stride) const {
@@ -1680,8 +1371,6 @@ struct Accum {
         int idx;
         if constexpr (MODE == NM_DENSE) {
             idx = x.c - colbase;
-        } else if constexpr (MODE == NM_RMAP) {
-            idx = rmap[x.c - colbase];  // one ds_read_u16
         } else {
             const int tc = x.c >> TILE_SHIFT;
             int s;
@@ -1854,7 +1543,7 @@ struct SymArgs {
     long long gbytes;  // per block
     unsigned long long* mcache;
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
-    int* cursors;            // all row cursors (slot NUM_NB + bin: MHS_DYN)
+    int* cursors;            // all row cursors (slot NUM_NB + bin: k_sym_rare queues)
     SpillLists sp;           // tile lists of rows past the row cache's cap
 };
 
@@ -1952,7 +1641,7 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
         }
     }
     // ... rows past the slot: a spill list (one copy for the group: lofs points every row at it)
-    if (MHS_SPILL && a.mcache && spill_row(span, tflop, t, a.mc_list)) {
+    if (a.mcache && spill_row(span, tflop, t, a.mc_list)) {
         const int off = spill_reserve(tm, a.sp, row, R, t);
         if (off >= 0) {
             // every wave compacts its share of the slots (the list is unordered): a wave
@@ -1994,11 +1683,6 @@ __device__ __forceinline__ void sym_wave_rows(const SymArgs& a, int bid, int nb)
     const int count = a.stats->sym_count[a.bin];
     const int* list = a.list + (long long)(a.bin - 1) * a.M;
     WaveTeam tm;
-    if (MHS_DYN > 0) {  // (the wave role's blocks are [0, nb) of the launch: bid = blockIdx)
-        WaveQueue q(a.cursors + (NUM_NB + a.bin) * 8 * CURSOR_STRIDE, count, MHS_DYN);
-        for (int li; q.next(li);) sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[li]), E, nullptr);
-        return;
-    }
     for (RowWalk rw(count, WPB, w, bid, nb); rw.first < rw.end; rw.first += rw.stride)
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, nullptr);
 }
@@ -2012,13 +1696,6 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
     const int count = a.stats->sym_count[a.bin];
     const int* list = a.list + (long long)(a.bin - 1) * a.M;
     int4* stage = (int4*)(smem + 1024);
-    if (MHS_BLKQ_SYMB) {
-        if (count == 0) return;  // (launched before the bin sizes are known: most calls have none)
-        __shared__ int qslot;
-        const BlockQueue q{a.cursors + (NUM_NB + a.bin) * 8 * CURSOR_STRIDE, &qslot, count};
-        for (int li; q.next(li);) sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[li]), E, stage);
-        return;
-    }
     for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride)
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, stage);
 }
@@ -2138,7 +1815,7 @@ __device__ bool sym_row_bitmap(const BlockTeam<1024, false>& tm, const SymArgs& 
                 st_cache(&slot[r], msk[r]);
                 st_cache(&reinterpret_cast<int*>(slot + a.mc_list)[r], kb[r].x);
             }
-    if (MHS_SPILL && a.mcache && spill_row(span, tflop, t, a.mc_list)) {  // in column order
+    if (a.mcache && spill_row(span, tflop, t, a.mc_list)) {  // in column order
         const int off = spill_reserve(tm, a.sp, row, R, t);
         if (off >= 0)
             for (int r = tm.rank(); r < t; r += T) {
@@ -2165,16 +1842,12 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
             const int span = __builtin_amdgcn_readfirstlane(a.rhi[row]) - __builtin_amdgcn_readfirstlane(a.rlo[row]) + 1;
             if (bin == SYM_B1024 && sym_direct(span, __builtin_amdgcn_readfirstlane(a.rtflop[row])))
                 sym_row(tm, a, row, E, stage);
-            else if (!(MHS_SPANRANK && sym_row_bitmap(tm, a, row, (char*)E, stage)))
+            else if (!sym_row_bitmap(tm, a, row, (char*)E, stage))
                 sym_row_wide(tm, a, row, (unsigned long long*)E, stage, (int*)(smem + 512));
         };
         if (count == 0) continue;  // (no atomics for an empty bin: most matrices have none)
-        if (MHS_BLKQ) {
-            const BlockQueue q{a.cursors + (NUM_NB + bin) * 8 * CURSOR_STRIDE, &qslot, count};
-            for (int li; q.next(li);) one(li);
-        } else {
-            for (RowWalk rw(count, 1, 0); rw.first < rw.end; rw.first += rw.stride) one(rw.first);
-        }
+        const BlockQueue q{a.cursors + (NUM_NB + bin) * 8 * CURSOR_STRIDE, &qslot, count};
+        for (int li; q.next(li);) one(li);
     }
     __syncthreads();  // phase 2 reuses the whole LDS
     const int w = threadIdx.x >> 6;
@@ -2296,9 +1969,6 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
     append_block_rows<SYM_NB, PER>(binof, M, stats->sym_count, list, (int)blockIdx.x);
 }
 
-#ifndef MHS_W16_BLOCK
-#define MHS_W16_BLOCK 0  // 1: rows of the 16 KiB wave bins go to the 256-thread block bin
-#endif
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
                                           int dense_span_max, int nA, bool tiny_ok) {
     if (n == 0) return NUM_NONE;
@@ -2310,7 +1980,7 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
     if (tc >= 0) return NUM_TINY + tc;  // a bigger table than the small wave bin's: sort in registers
     if (num_wide(span, t, n, dense_span_max) || num_ranked(span, t, n, dense_span_max))
         return NUM_B1024;  // rank by span bitmap, else windowed masks with global accumulation
-    if (!MHS_W16_BLOCK && need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return hash ? NUM_W16H : NUM_W16;
+    if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return hash ? NUM_W16H : NUM_W16;
     if (need <= NUM_B256_BYTES - BLOCK_HDR && flop <= NUM_B256_WORK) return NUM_B256;
     if (need <= B1024_BYTES) return NUM_B1024;
     atomicMax(gneed, (int)(need > INT_MAX ? INT_MAX : need));
@@ -2528,40 +2198,10 @@ struct NumArgs {
     int dense_span_max;
     const unsigned long long* mcache;
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
-    int* cursor;             // this launch's 8 row cursors (MHS_DYN)
+    int* cursor;             // this launch's row cursors (block queue, guided / queued wave walks)
     SpillLists sp;           // tile lists of rows past the row cache's cap (symbolic -> numeric)
     int qall;                // guided bins: every row from the cursor (few rows a wave)
 };
-
-#ifndef MHS_RANK_SORT
-#define MHS_RANK_SORT 0  // register-sort ranking: measured cage15-like +3 %, offshore +2 % (kept off)
-#endif
-constexpr int RANK_SORT_MIN = 32;  // tiles below which counting is as cheap
-// Tile bases of a hashed wave row from its compacted (key, slot << 8 | popc) list L of t
-// tiles (t <= 64 K, keys within 2^23 of lo, slots < 512): E[slot].base = the popcounts of
-// the smaller keys.
-template <int K>
-__device__ __forceinline__ void rank_sorted(TileEntry* E, const int2* L, int t, int lo) {
-    const int lane = lane_id();
-    unsigned k[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        const int e = i * 64 + lane;
-        const int2 v = e < t ? L[e] : make_int2(0, 0);
-        k[i] = e < t ? ((unsigned)(v.x - lo) << 9) | (unsigned)(v.y >> 8) : 0xFFFFFFFFu;
-    }
-    reg_bitonic<64, K>(k, lane);
-    int carry = 0;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        const bool real = k[i] != 0xFFFFFFFFu;
-        const int slot = (int)(k[i] & 511u);
-        const int p = real ? (int)__popcll(E[slot].mask) : 0;
-        const int inc = wave_incl_scan(p);
-        if (real) E[slot].base = carry + inc - p;
-        carry += __shfl(inc, 63);
-    }
-}
 
 template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
 __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, int span, int t,
@@ -2571,9 +2211,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     const int H = MODE == NM_HASH ? hash_slots(t) : span;
     const int colbase = lo << TILE_SHIFT;
     TileEntry* E = (TileEntry*)region;
-    unsigned short* rmap = (unsigned short*)(region + (long long)H * 16);
-    double* acc = (double*)(region + (long long)H * 16 +
-                            (MODE == NM_RMAP ? align16((long long)span * TILE_BITS * 2) : 0));
+    double* acc = (double*)(region + (long long)H * 16);
     const int nacc = MODE == NM_DENSE ? span * TILE_BITS : n;
     const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
     // row group: R accumulator slices `stride` doubles apart; C row r at c0 + r*n
@@ -2586,7 +2224,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     // symbolic kept the masks unless it sorted the row as a tiny one (numeric runs those
     // with tables when the tiny classes are off: N beyond the packed keys' 23 bits)
     const bool sym_tiny = tiny_class_sym(__builtin_amdgcn_readfirstlane(a.rflop[row]), a1 - a0) >= 0;
-    const int lofs = (MHS_SPILL && a.mcache && !sym_tiny && spill_row(span, tflop, t, a.mc_list))
+    const int lofs = (a.mcache && !sym_tiny && spill_row(span, tflop, t, a.mc_list))
                          ? __builtin_amdgcn_readfirstlane(a.sp.lofs[row])
                          : -1;
     // hashed rows rank their tiles by a bitmap over the span (block teams / many tiles,
@@ -2703,18 +2341,10 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
                     make_int2((int)q.w, (s << 8) | __popcll(((unsigned long long)q.y << 32) | q.x));
         }
         tm.sync();
-        if (Team::size == 64 && MHS_RANK_SORT && t > RANK_SORT_MIN && t <= 256 && span <= (1 << 23) && H <= 512) {
-            // wave teams, more than a few dozen tiles: sort (key offset << 9 | slot) in
-            // registers (bitonic over DPP, K = 1 / 2 / 4 keys per lane), then the bases are an
-            // exclusive scan of the popcounts in sorted order -- O(t log^2 t / 64) per lane
-            // instead of the count's t^2 / 64
-            if (t <= 64) rank_sorted<1>(E, L, t, lo);
-            else if (t <= 128) rank_sorted<2>(E, L, t, lo);
-            else rank_sorted<4>(E, L, t, lo);
-        } else
+        // (sorting the keys in registers instead -- bitonic over DPP -- measured cage15-like +3 %)
         for (int i = tm.rank(); i < t; i += Team::size) {
             const int2 me = L[i];
-            int base = 0, j = MHS_NUM_DIAG == 10 ? t : 0;  // diag 10: ranking skipped (timing only)
+            int base = 0, j = 0;
             for (; j + 1 < t; j += 2) {  // two entries per broadcast read
                 const int4 o = *reinterpret_cast<const int4*>(&L[j]);
                 base += (o.x < me.x ? (o.y & 0xFF) : 0) + (o.z < me.x ? (o.w & 0xFF) : 0);
@@ -2743,17 +2373,6 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
             [&](int e, int v) { E[(int)(unsigned)S[e]].base = v; });
     }
     tm.sync();
-    if constexpr (MODE == NM_RMAP) {
-        // column -> C-row rank over the span (one wave per tile, lane = bit)
-        const int lane = lane_id();
-        const int nw = Team::size / 64, wv = tm.rank() >> 6;
-        for (int s = wv; s < span; s += nw) {
-            const TileEntry e = E[s];
-            if ((e.mask >> lane) & 1ull)
-                rmap[(s << TILE_SHIFT) + lane] = (unsigned short)(e.base + __popcll(e.mask & lanemask_lt()));
-        }
-        tm.sync();
-    }
     MHS_STAMP(2);
     for (int r = tm.rank(); r < nclear; r += Team::size) acc[r] = 0.0;
     tm.sync();
@@ -2761,7 +2380,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
 
     // 3. accumulate every product of the row (of the group's rows)
     {
-        const Accum<GLOBALMEM, MODE> f{E, acc, rmap, lo, H, colbase, a.Bcol, a.Bval};
+        const Accum<GLOBALMEM, MODE> f{E, acc, lo, H, colbase, a.Bcol, a.Bval};
         if constexpr (GROUPED)
             for_products_group(a0, a1, a.Acol, a.Aval, a.bmeta, pick_group(a.rflop[row], a1 - a0, 64), f, R,
                                a1 - a0, stride);
@@ -2978,7 +2597,7 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
     int2* kb = (int2*)(region + sb + align16((long long)t * 8));
     double* acc = (double*)(region + sb + 2 * align16((long long)t * 8));
     const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
-    const int lofs = (MHS_SPILL && a.mcache && spill_row(span, tflop, t, a.mc_list))
+    const int lofs = (a.mcache && spill_row(span, tflop, t, a.mc_list))
                          ? __builtin_amdgcn_readfirstlane(a.sp.lofs[row])
                          : -1;
     for (int i = tm.rank(); i < nw; i += T) bm[i] = 0ull;
@@ -3058,8 +2677,6 @@ __device__ void num_row(const Team& tm, const NumArgs& a, int row, char* region,
     }
     if (mode == NM_DENSE)
         num_row_body<Team, GLOBALMEM, NM_DENSE, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
-    else if (mode == NM_RMAP)
-        num_row_body<Team, GLOBALMEM, NM_RMAP, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else if (MODES == MODES_NOHASH || mode == NM_DIRECT)
         num_row_body<Team, GLOBALMEM, NM_DIRECT, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else
@@ -3090,8 +2707,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     // bin guided with half static: wb-edu-like numeric -4 %, webbase-like -2 %, cage15-like and
     // pdb1HYS-like neutral; the whole bin from the cursor (2 rows a take): wb-edu -12 %,
     // webbase -10 %, but cage15 +3.5 %; the direct / grouped 16 KiB bins guided: pdb1HYS +10 %.
-    constexpr bool guided = MHS_DYN == 0 && BYTES == NUM_W16_BYTES &&
-                            ((HASH && (MHS_GUIDED16 & 1)) || (!HASH && (MHS_GUIDED16 & 2)));
+    constexpr bool guided = BYTES == NUM_W16_BYTES && HASH;
     if (guided && a.qall) {
         WaveQueue q(a.cursor, a.count, 1);
         for (int li; q.next(li);) one(li);
@@ -3109,9 +2725,6 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
             if (li >= end) break;
             one(li);
         }
-    } else if (MHS_DYN > 0) {
-        WaveQueue q(a.cursor, a.count, MHS_DYN);
-        for (int li; q.next(li);) one(li);
     } else {
         for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride) one(rw.first);
     }
@@ -3143,15 +2756,7 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
     int4* stage = (int4*)(smem + 1024);
     __shared__ int qslot;
     const BlockQueue q{a.cursor, &qslot, a.count};
-    RowWalk rw(a.count, 1, 0);
-    for (int li;;) {
-        if (MHS_BLKQ_NUM) {
-            if (!q.next(li)) break;
-        } else {
-            if (rw.first >= rw.end) break;
-            li = rw.first;
-            rw.first += rw.stride;
-        }
+    for (int li; q.next(li);) {
         const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
         if constexpr (T == 1024 && !GLOBALMEM) {
             const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
@@ -3159,7 +2764,7 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
             const int t = __builtin_amdgcn_readfirstlane(a.ctiles[row]);
             const int c0 = __builtin_amdgcn_readfirstlane(a.Cptr[row]);
             const int n = __builtin_amdgcn_readfirstlane(a.Cptr[row + 1]) - c0;
-            if (MHS_SPANRANK && num_ranked(hi - lo + 1, t, n, a.dense_span_max)) {
+            if (num_ranked(hi - lo + 1, t, n, a.dense_span_max)) {
                 num_row_bitmap<T>(tm, a, row, lo, hi - lo + 1, t, c0, n, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
                                   __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]), reg, stage);
                 continue;
@@ -3420,10 +3025,7 @@ __device__ __forceinline__ void tiny_sym_rows(TinyArgs a, int blk) {
 }
 
 // Numeric-first rows: C entries from their value slots, L lanes per row (two entries
-// per lane in flight), class c's list over blocks [f.blk0[k], f.blk0[k+1]).
-#ifndef MHS_COPY_ROWS
-#define MHS_COPY_ROWS 1
-#endif
+// per lane in flight).
 struct CopyArgs {
     const int* list;  // numeric bin lists (class c's at (NUM_TINY + c - 1) * M)
     long long M;
@@ -3434,46 +3036,12 @@ struct CopyArgs {
     int* Ccol;
     double* Cval;
 };
-template <int L>
-__device__ __forceinline__ void copy_rows(const CopyArgs& a, const int* list, int count, int bid, int nb) {
-    const int tl = threadIdx.x & (L - 1);
-    for (int it = bid * (256 / L) + (int)(threadIdx.x / L); it < count; it += nb * (256 / L)) {
-        const int row = list[it];
-        const int c0 = a.Cptr[row], n = a.Cptr[row + 1] - c0;
-        const long long src = a.tslot[row];
-        for (int k = tl; k < n; k += 2 * L) {
-            const bool two = k + L < n;
-            const int x0 = a.sc_col[src + k];
-            const double v0 = a.sc_val[src + k];
-            const int x1 = two ? a.sc_col[src + k + L] : 0;
-            const double v1 = two ? a.sc_val[src + k + L] : 0.0;
-            a.Ccol[c0 + k] = x0;
-            a.Cval[c0 + k] = v0;
-            if (two) {
-                a.Ccol[c0 + k + L] = x1;
-                a.Cval[c0 + k + L] = v1;
-            }
-        }
-    }
-}
-__global__ __launch_bounds__(256) void k_tiny_copy(CopyArgs a, TinyFused f) {
-    int k = 0;
-    while (k + 1 < f.nclass && (int)blockIdx.x >= f.blk0[k + 1]) ++k;
-    const int bid = (int)blockIdx.x - f.blk0[k], nb = f.blk0[k + 1] - f.blk0[k];
-    const int c = f.c[k], count = f.count[k];
-    const int* list = a.list + (long long)(NUM_TINY + c - 1) * a.M;
-    switch (c) {  // lanes per row ~ a quarter of the class's products
-    case 0: copy_rows<4>(a, list, count, bid, nb); break;
-    case 1: copy_rows<8>(a, list, count, bid, nb); break;
-    case 2: copy_rows<16>(a, list, count, bid, nb); break;
-    default: copy_rows<32>(a, list, count, bid, nb); break;
-    }
-}
 static int copy_lanes(int c) { return c == 0 ? 4 : c == 1 ? 8 : c == 2 ? 16 : 32; }
 
-// The same in row order (MHS_COPY_ROWS): L lanes per row over every row of A, slot rows
-// only (tslot >= 0; k_scan marks the others): a wave's stores cover consecutive C rows
-// and its loads consecutive slots, with no list in the chain.
+// In row order: L lanes per row over every row of A, slot rows only (tslot >= 0; k_scan
+// marks the others): a wave's stores cover consecutive C rows and its loads consecutive
+// slots, with no list in the chain (measured: GAP-road-like copy 1.44 -> 0.82 ms against
+// walking each class's list).
 template <int L>
 __global__ __launch_bounds__(256) void k_tiny_copy_rows(CopyArgs a) {
     const int tl = threadIdx.x & (L - 1);
@@ -3559,11 +3127,9 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
 }
 
 // k_analyze: G lanes per row, 256-thread blocks.
-#ifndef MHS_AN_G2
-#define MHS_AN_G2 1  // 2-lane groups for rows of < 3 entries on average (GAP-road-like 5.29 -> 4.97 ms)
-#endif
+// 2-lane groups for rows of < 3 entries on average (GAP-road-like 5.29 -> 4.97 ms)
 static void analyze_geometry(long long nnzA, int M, int* G, int* blocks) {
-    *G = MHS_AN_G2 && M > 0 && nnzA / M < 3 ? 2 : pick_group(nnzA, M, MHS_AN_GMAX);
+    *G = M > 0 && nnzA / M < 3 ? 2 : pick_group(nnzA, M, MHS_AN_GMAX);
     const int rpb = 256 / *G;
     *blocks = (M + rpb - 1) / rpb;
 }
@@ -3764,12 +3330,9 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
 }
 
 // Dynamic LDS of a block-kernel launch: the header plus its largest row's tables, in
-// 2 KiB steps, at most the bin's budget (MHS_BLOCK_LDS_FIXED=1: always the budget).
-#ifndef MHS_BLOCK_LDS_FIXED
-#define MHS_BLOCK_LDS_FIXED 0
-#endif
+// 2 KiB steps, at most the bin's budget.
 static int block_lds(int need, int budget) {
-    if (MHS_BLOCK_LDS_FIXED || need <= 0) return budget;
+    if (need <= 0) return budget;
     const int b = (BLOCK_HDR + need + 2047) & ~2047;
     return b < budget ? b : budget;
 }
@@ -3851,15 +3414,12 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         if (f.nclass > 0) {
             const CopyArgs ca{w.bin_list, A.M, Cptr, w.tslot, w.sc_col, w.sc_val, Ccol, Cval};
             s = next_stream();
-            if (MHS_COPY_ROWS) {  // lanes per row by the median row's class
-                const int L = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
-                const dim3 grid(round8((A.M + 256 / L - 1) / (256 / L), 16384));
-                if (L == 4) hipLaunchKernelGGL(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
-                else if (L == 8) hipLaunchKernelGGL(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
-                else hipLaunchKernelGGL(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
-            } else {
-                hipLaunchKernelGGL(k_tiny_copy, dim3(f.blk0[f.nclass]), dim3(256), 0, s, ca, f);
-            }
+            // lanes per row by the median row's class
+            const int L = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
+            const dim3 grid(round8((A.M + 256 / L - 1) / (256 / L), 16384));
+            if (L == 4) hipLaunchKernelGGL(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
+            else if (L == 8) hipLaunchKernelGGL(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
+            else hipLaunchKernelGGL(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
         }
     }
     // Largest bins first so the long rows start early.
