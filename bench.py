@@ -161,12 +161,26 @@ def main():
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     N_GPUS = world
+    # MHS_BENCH_BACKEND=gloo: a rehearsal of the N > 1 path on a one-GPU box (every rank on
+    # cuda:0, the exchange over gloo on host tensors) -- never a measurement
+    backend = os.environ.get("MHS_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    T_START = time.time()
+
+    def log(msg):  # progress on stderr (rank 0): long N > 1 setups stay visible
+        if rank == 0:
+            print(f"[bench {time.time() - T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
     if args.matrix is None:
         args.matrix = "cant" if world == 1 else "cage15"
@@ -182,11 +196,13 @@ def main():
             synth.build_shared(args.matrix)
         dist.barrier()
         M_glob, N_glob, s_ptr, s_col, s_val, source = synth.open_shared(args.matrix)
+        log(f"{args.matrix}: {M_glob} rows, shared host copy ready")
         nnzA = int(s_ptr[-1])
         flop = mhspgemm.flop_count_np(s_col, s_ptr) if rank == 0 else 0
     tool = mhspgemm.Tool(local)
     tool.set_stream(torch.cuda.current_stream(local).cuda_stream)
     dev = f"cuda:{local}"
+    xdev = "cpu" if backend == "gloo" else dev  # where the exchange's tensors live
 
     def barrier():
         if dist is not None:
@@ -259,6 +275,7 @@ def main():
             ms1 = (time.perf_counter() - t0) / args.steps * 1e3
             one_gpu = {"ms_per_step": round(ms1, 4), "value": round(2.0 * flop / (ms1 * 1e-3) / 1e9, 2),
                        "note": "the same matrix, whole, on rank 0's GPU alone (same steps / warmup)"}
+            log(f"one-GPU leg: {ms1:.3f} ms per step")
             t1.close()
             A1.release()
             del A1
@@ -269,7 +286,7 @@ def main():
         # of the file would hold); the flop balance and the exchange plan are built from the
         # blocks with collectives, timed as plan_ms (setup, outside the steps)
         r0, r1 = D.equal_rows(M_glob, world, rank)
-        eq = D.local_block(s_ptr, s_col, s_val, r0, r1, dev)
+        eq = D.local_block(s_ptr, s_col, s_val, r0, r1, xdev)
         del s_col, s_val
         barrier()
         p0 = time.perf_counter()
@@ -278,7 +295,14 @@ def main():
         plan = D.ShardPlan(blk, M_glob, mode=args.exchange)
         barrier()
         plan_ms = (time.perf_counter() - p0) * 1e3
+        log(f"plan built in {plan_ms:.0f} ms")
         mult = D.hip_local_multiply(tool)
+        if xdev != dev:  # rehearsal: the exchanged rows go to the GPU for the HIP multiply
+            hip_mult = mult
+
+            def mult(A, Bp, Bc, Bv, N):
+                Ag = D.Block(A.r0, A.r1, A.ptr.to(dev), A.col.to(dev), A.val.to(dev))
+                return hip_mult(Ag, Bp.to(dev), Bc.to(dev), Bv.to(dev), N)
 
         def timed(pl):
             for _ in range(args.warmup):
@@ -292,13 +316,14 @@ def main():
                 nloc = C.nnz
                 C.release()
             barrier()
-            tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=xdev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            nn = torch.tensor([nloc, pl.bytes_in, pl.nB], dtype=torch.int64, device=dev)
+            nn = torch.tensor([nloc, pl.bytes_in, pl.nB], dtype=torch.int64, device=xdev)
             dist.all_reduce(nn)
             return float(tt.item()), [int(x) for x in nn.tolist()]
 
         t_max, (nnzC, xbytes, xrows) = timed(plan)
+        log(f"{args.exchange} steps: {t_max / args.steps * 1e3:.3f} ms per step")
         # the other exchange mode beside it (the north_star's allgatherv when the headline is halo)
         alt_mode = "full" if args.exchange == "halo" else "halo"
         alt_plan = D.ShardPlan(blk, M_glob, mode=alt_mode)
@@ -309,7 +334,7 @@ def main():
             C, _ = D.spgemm_planned(plan, mult)
             barrier()
             g0 = time.perf_counter()
-            D.gather_result(C, blk)
+            D.gather_result(C if xdev == dev else tuple(x.cpu() for x in C.to_torch()), blk)
             barrier()
             gather_ms = (time.perf_counter() - g0) * 1e3
             C.release()
@@ -340,7 +365,8 @@ def main():
             "workload": f"{args.matrix}.mtx A*A ({source}), device-resident A -> device-resident sorted C",
             "matrix": args.matrix, "rows": M_glob, "nnzA": nnzA, "flop": flop, "nnzC": nnzC,
             "parallelism": "single GPU" if N_GPUS == 1 else
-                           f"row-sharded x{N_GPUS}, {args.exchange} exchange of B's rows in every step, C distributed",
+                           f"row-sharded x{N_GPUS}, {args.exchange} exchange of B's rows in every step, C distributed"
+                           + (" [gloo rehearsal on one GPU: not a measurement]" if backend == "gloo" else ""),
             "memory": "steady-state steps reuse the context's workspace and pooled C buffers "
                       "(no hipMalloc in a step); cold_call times a fresh context",
         },

@@ -343,6 +343,9 @@ struct RowWalk {
     }
 };
 
+#ifndef MHS_PRESTAGE
+#define MHS_PRESTAGE 0  // wave numeric rows: stage the first A chunk before the tile table
+#endif
 #ifndef MHS_GRP_CHUNK
 #define MHS_GRP_CHUNK 63  // A entries staged per chunk in the grouped walk (<= 64)
 #endif
@@ -1059,12 +1062,9 @@ __device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int 
 
 // One wave's chunks of an A row: [jb0, jb0 + 64), [jb0 + jstep, ...), ... below a1.
 template <class F>
-__device__ __forceinline__ void wave_chunks(int jb0, int jstep, int a1, const int* __restrict__ Acol,
-                                            const double* __restrict__ Aval, const int4* __restrict__ bmeta,
-                                            bool tiles, int Grow, const F& f) {
+__device__ __forceinline__ void wave_chunk(const StagedChunk& x, int Grow, const F& f) {
     const int lane = lane_id();
-    for (int jb = jb0; jb < a1; jb += jstep) {
-        const StagedChunk x = stage_chunk(lane, jb, a1, Acol, Aval, bmeta, tiles);
+    {
         // a chunk with merged runs loads LM rows per lane and sweep: wider groups
         // keep each load instruction within fewer cache lines
         const int G = (F::kValues && x.lmax > 1 && Grow < MHS_RUN_GMIN) ? MHS_RUN_GMIN : Grow;
@@ -1102,6 +1102,13 @@ __device__ __forceinline__ void wave_chunks(int jb0, int jstep, int a1, const in
             }
         }
     }
+}
+template <class F>
+__device__ __forceinline__ void wave_chunks(int jb0, int jstep, int a1, const int* __restrict__ Acol,
+                                            const double* __restrict__ Aval, const int4* __restrict__ bmeta,
+                                            bool tiles, int Grow, const F& f) {
+    for (int jb = jb0; jb < a1; jb += jstep)
+        wave_chunk(stage_chunk(lane_id(), jb, a1, Acol, Aval, bmeta, tiles), Grow, f);
 }
 
 
@@ -2217,6 +2224,12 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     // row group: R accumulator slices `stride` doubles apart; C row r at c0 + r*n
     const int stride = GROUPED ? (int)(num_acc_bytes(MODE, span, t, n) / 8) : 0;
     const int nclear = GROUPED ? (R - 1) * stride + nacc : nacc;
+    // Wave rows: the row's first chunk of A entries (A.col, A.val -> bmeta) is loaded before
+    // the tile table is built, so its two dependent global round trips overlap the table's
+    // LDS work instead of following it
+    constexpr bool PRE = MHS_PRESTAGE && Team::size == 64 && !GROUPED;
+    StagedChunk x0{};
+    if constexpr (PRE) x0 = stage_chunk(lane_id(), a0, a1, a.Acol, a.Aval, a.bmeta, false);
 
     // 1. the C row's tile table: the symbolic pass's masks when it kept them,
     //    else rebuilt (same OR pass as symbolic)
@@ -2381,11 +2394,16 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     // 3. accumulate every product of the row (of the group's rows)
     {
         const Accum<GLOBALMEM, MODE> f{E, acc, lo, H, colbase, a.Bcol, a.Bval};
-        if constexpr (GROUPED)
+        if constexpr (GROUPED) {
             for_products_group(a0, a1, a.Acol, a.Aval, a.bmeta, pick_group(a.rflop[row], a1 - a0, 64), f, R,
                                a1 - a0, stride);
-        else
+        } else if constexpr (PRE) {
+            const int G = pick_group(a.rflop[row], a1 - a0, 64, MHS_VAL_GMIN, MHS_UNROLL);
+            wave_chunk(x0, G, f);
+            wave_chunks(a0 + 64, 64, a1, a.Acol, a.Aval, a.bmeta, false, G, f);
+        } else {
             walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
+        }
     }
     tm.sync();
     MHS_STAMP(4);

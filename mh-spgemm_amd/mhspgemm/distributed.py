@@ -77,8 +77,9 @@ def local_block(ptr: np.ndarray, col: np.ndarray, val: np.ndarray, r0: int, r1: 
     import torch
     s, e = int(ptr[r0]), int(ptr[r1])
     p = torch.from_numpy((ptr[r0:r1 + 1].astype(np.int64) - s).astype(np.int32)).to(device)
-    return Block(r0, r1, p, torch.from_numpy(np.ascontiguousarray(col[s:e])).to(device),
-                 torch.from_numpy(np.ascontiguousarray(val[s:e])).to(device))
+    # np.array copies: the inputs may be read-only memory maps (bench.py's shared host copy)
+    return Block(r0, r1, p, torch.from_numpy(np.array(col[s:e], dtype=np.int32)).to(device),
+                 torch.from_numpy(np.array(val[s:e], dtype=np.float64)).to(device))
 
 
 def equal_rows(M: int, P: int, p: int):

@@ -1,5 +1,6 @@
-"""Per-phase cycle totals of numeric rows (diag build 9), heads only, plus occupancy math."""
-import sys, ctypes, os
+"""Per-phase cycle totals of numeric rows (MHS_ROW_STAMPS build in tools/diag/v9), heads
+only.  usage: python tools/diag/stamps2.py <matrix>   (prints progress: long runs stay visible)"""
+import sys, ctypes, os, time
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "mh-spgemm_amd")]
@@ -8,37 +9,39 @@ import numpy as np, torch
 from mhspgemm import _lib
 import mhspgemm
 from mhspgemm import synth
-A = synth.SYNTH[sys.argv[1] if len(sys.argv) > 1 else "cant"](); A.H2D(0)
+t0 = time.time()
+name = sys.argv[1] if len(sys.argv) > 1 else "cant"
+A, _ = synth.load_or_synth(name)
+print(f"[{time.time()-t0:.1f}s] matrix {name} rows {A.M}", flush=True)
+A.H2D(0)
 tool = mhspgemm.Tool(0)
 L = _lib.lib(); L.mhs_diag_setup.argtypes = [ctypes.c_int, ctypes.c_void_p]
 dev = ctypes.c_void_p()
 assert L.mhs_diag_setup(A.M, ctypes.byref(dev)) == 0
 for i in range(3):
     C, t = mhspgemm.spgemm(tool, A, A); C.release()
+    print(f"[{time.time()-t0:.1f}s] call {i}: numeric {t.Numeric:.3f} ms", flush=True)
 buf = np.zeros(A.M * 8, np.uint64)
-L.mhs_memcpy(tool.ctx, buf.ctypes.data, dev, buf.nbytes, 1)
+assert L.mhs_memcpy(tool.ctx, ctypes.c_void_p(buf.ctypes.data), dev, buf.nbytes, 1) == 0
 ph = buf.reshape(A.M, 8).astype(np.float64)
 heads = ph[:, :6].sum(1) > 0
-names = ["prologue", "tiles(load/build)", "bases(+rmap)", "clear_acc", "accumulate", "output"]
-print("heads", heads.sum(), "of", A.M)
+names = ["prologue", "tiles(load/build)", "bases", "clear_acc", "accumulate", "output"]
+print("heads", heads.sum(), "of", A.M, flush=True)
 for k, nm in enumerate(names):
     print(f"{nm:20s} {ph[heads, k].mean():10.0f} cycles/head")
 tot = ph[heads, :6].sum()
 print("sum cycles over heads %.3e ; numeric ms %.4f" % (tot, t.Numeric))
-# the slowest rows (top 1% by total cycles): where their time goes
 tot_r = ph[:, :6].sum(1)
 thr = np.percentile(tot_r[heads], 99)
 slow = heads & (tot_r >= thr)
 print("slowest 1%% rows: %d rows, mean total %.0f cycles" % (slow.sum(), tot_r[slow].mean()))
 for k, nm in enumerate(names):
     print(f"  {nm:20s} {ph[slow, k].mean():10.0f} cycles/row")
-# the bulk: rows between the 25th and 75th percentile of total cycles
 lo_, hi_ = np.percentile(tot_r[heads], [25, 75])
 mid = heads & (tot_r >= lo_) & (tot_r <= hi_)
 print("middle 50%% rows: %d rows, mean total %.0f cycles" % (mid.sum(), tot_r[mid].mean()))
 for k, nm in enumerate(names):
     print(f"  {nm:20s} {ph[mid, k].mean():10.0f} cycles/row")
-# rows grouped by product count (flop) bucket
 blen = np.diff(A.ptr).astype(np.int64)
 rf = np.add.reduceat(blen[A.col], A.ptr[:-1]) * (np.diff(A.ptr) > 0)
 edges = [0, 256, 1024, 2048, 4096, 8192, 1 << 40]
