@@ -343,9 +343,6 @@ struct RowWalk {
     }
 };
 
-#ifndef MHS_PRESTAGE
-#define MHS_PRESTAGE 0  // wave numeric rows: stage the first A chunk before the tile table
-#endif
 #ifndef MHS_GRP_CHUNK
 #define MHS_GRP_CHUNK 63  // A entries staged per chunk in the grouped walk (<= 64)
 #endif
@@ -2224,12 +2221,6 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     // row group: R accumulator slices `stride` doubles apart; C row r at c0 + r*n
     const int stride = GROUPED ? (int)(num_acc_bytes(MODE, span, t, n) / 8) : 0;
     const int nclear = GROUPED ? (R - 1) * stride + nacc : nacc;
-    // Wave rows: the row's first chunk of A entries (A.col, A.val -> bmeta) is loaded before
-    // the tile table is built, so its two dependent global round trips overlap the table's
-    // LDS work instead of following it
-    constexpr bool PRE = MHS_PRESTAGE && Team::size == 64 && !GROUPED;
-    StagedChunk x0{};
-    if constexpr (PRE) x0 = stage_chunk(lane_id(), a0, a1, a.Acol, a.Aval, a.bmeta, false);
 
     // 1. the C row's tile table: the symbolic pass's masks when it kept them,
     //    else rebuilt (same OR pass as symbolic)
@@ -2397,10 +2388,6 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
         if constexpr (GROUPED) {
             for_products_group(a0, a1, a.Acol, a.Aval, a.bmeta, pick_group(a.rflop[row], a1 - a0, 64), f, R,
                                a1 - a0, stride);
-        } else if constexpr (PRE) {
-            const int G = pick_group(a.rflop[row], a1 - a0, 64, MHS_VAL_GMIN, MHS_UNROLL);
-            wave_chunk(x0, G, f);
-            wave_chunks(a0 + 64, 64, a1, a.Acol, a.Aval, a.bmeta, false, G, f);
         } else {
             walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
         }
