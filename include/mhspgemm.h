@@ -100,10 +100,12 @@ int mhs_ctx_trim(mhs_ctx *ctx);
  *     on, rows of at most 128 products are summed during the symbolic phase into
  *     cached value slots and numeric only copies them into C (one sort instead of
  *     two; one more device-to-host hand-off per call, so big matrices only).
- * Out of memory: when the workspace, or C beside it, does not fit, mhs_spgemm gives
- * back every cached buffer and retries row-chunked (the workspace sized for half the
- * rows, halved until it fits; C sized by a counting pass and allocated once); it
- * returns MHS_ERR_OOM only when C itself or a one-row workspace does not fit. */
+ * Out of memory: when the workspace, C.ptr, the global-bin scratch or C beside them does
+ * not fit, mhs_spgemm gives back every cached buffer and retries row-chunked: a counting
+ * pass with the largest chunk workspace that fits sizes C; C is allocated before the
+ * second pass's workspace (halved only while that workspace does not fit beside C).  It
+ * returns MHS_ERR_OOM right after the counting pass when C itself does not fit, or when
+ * a one-row workspace does not fit. */
 typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2, MHS_OPT_MEM_BUDGET = 3,
                            MHS_OPT_TINY_FIRST_ROWS = 4 } mhs_option;
 int mhs_ctx_set_option(mhs_ctx *ctx, int option, int value);

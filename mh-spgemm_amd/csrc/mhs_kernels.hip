@@ -269,28 +269,42 @@ struct StagedChunk {
 };
 
 // Lanes hold the chunk entries [jb, jb+64) ∩ [.., a1) of one A row (lane 0 = jb).
-// Loads are issued together (kprev clamped, not branched on) and every lane
-// reaches the ballots.
-__device__ __forceinline__ StagedChunk stage_chunk(int lane, int jb, int a1,
-                                                   const int* __restrict__ Acol,
-                                                   const double* __restrict__ Aval,
-                                                   const int4* __restrict__ bmeta, bool tiles) {
-    StagedChunk x;
-    x.st = 0;
-    x.ln = 0;
-    x.av = 0.0;
+// Staging is split in its loads (ChunkLoads: A.col, the previous A.col, A.val, then
+// bmeta of the column) and the ballots that turn them into visits (finish_chunk), so a
+// walk can issue the loads of its next chunk before it walks the current one.  Loads are
+// issued together (kprev clamped, not branched on) and every lane reaches the ballots.
+struct ChunkLoads {
+    int k, kp;
+    int4 m;
+    double av;
+    bool in;
+};
+__device__ __forceinline__ ChunkLoads load_chunk_a(int lane, int jb, int a1, const int* __restrict__ Acol,
+                                                   const double* __restrict__ Aval) {
+    ChunkLoads c;
     const int jl = jb + lane;
-    const bool in = jl < a1;
-    bool cont = false;
-    if (in) {
-        const int k = Acol[jl];
-        const int kp = Acol[jl > 0 ? jl - 1 : 0];
-        const int4 m = bmeta[k];
-        x.st = m.x;
-        x.ln = tiles ? meta_ntiles(m) : m.y;
-        cont = lane > 0 && meta_same(m) && kp == k - 1;
-        if (Aval) x.av = Aval[jl];
+    c.in = jl < a1;
+    c.k = 0;
+    c.kp = 0;
+    c.av = 0.0;
+    c.m = make_int4(0, 0, 0, 0);
+    if (c.in) {
+        c.k = Acol[jl];
+        c.kp = Acol[jl > 0 ? jl - 1 : 0];
+        if (Aval) c.av = Aval[jl];
     }
+    return c;
+}
+__device__ __forceinline__ void load_chunk_meta(ChunkLoads& c, const int4* __restrict__ bmeta) {
+    if (c.in) c.m = bmeta[c.k];
+}
+__device__ __forceinline__ StagedChunk finish_chunk(int lane, const ChunkLoads& c, bool tiles) {
+    StagedChunk x;
+    x.st = c.in ? c.m.x : 0;
+    x.ln = c.in ? (tiles ? meta_ntiles(c.m) : c.m.y) : 0;
+    x.av = c.av;
+    const bool in = c.in;
+    const bool cont = in && lane > 0 && meta_same(c.m) && c.kp == c.k - 1;
     const unsigned long long C = __ballot(cont);
     bool head;
     if (tiles) {
@@ -319,6 +333,30 @@ __device__ __forceinline__ StagedChunk stage_chunk(int lane, int jb, int a1,
     }
     x.lmax = lm;
     return x;
+}
+__device__ __forceinline__ StagedChunk stage_chunk(int lane, int jb, int a1,
+                                                   const int* __restrict__ Acol,
+                                                   const double* __restrict__ Aval,
+                                                   const int4* __restrict__ bmeta, bool tiles) {
+    ChunkLoads c = load_chunk_a(lane, jb, a1, Acol, Aval);
+    load_chunk_meta(c, bmeta);
+    return finish_chunk(lane, c, tiles);
+}
+
+// Lane-group width of one staged chunk: nh visits of about `avg` B entries each, U entries
+// per lane and load batch.  Minimises the chunk's dependent load batches
+// ceil(nh / groups) * ceil(avg / (G*U)), ties to the wider group; at least gmin.
+__device__ __forceinline__ int chunk_group(int nh, int avg, int U, int gmin) {
+    int best = gmin, bc = INT_MAX;
+    for (int g = gmin; g <= 64; g <<= 1) {
+        const int ng = 64 / g;
+        const int c = ((nh + ng - 1) / ng) * ((avg + g * U - 1) / (g * U));
+        if (c <= bc) {
+            bc = c;
+            best = g;
+        }
+    }
+    return best;
 }
 
 // XCD-grouped walk over a row list: blocks b and b+8 share an XCD (round-robin
@@ -1109,6 +1147,32 @@ __device__ __forceinline__ void wave_chunks(int jb0, int jstep, int a1, const in
 }
 
 
+// A wave's row walk with chunks staged in pairs (as for_products_group) and a lane-group
+// width per chunk (chunk_group): a row's short last chunk takes wide groups.
+#ifndef MHS_WAVE_PAIRS
+#define MHS_WAVE_PAIRS 1
+#endif
+template <class F>
+__device__ __forceinline__ void wave_walk(int a0, int a1, const int* __restrict__ Acol, const double* __restrict__ Aval,
+                                          const int4* __restrict__ bmeta, bool tiles, long long work, const F& f) {
+    const int lane = lane_id();
+    const int nA = a1 - a0;
+    const int avg = nA > 0 ? (int)((work + nA - 1) / nA) : 1;
+    const int U = tiles ? 1 : MHS_UNROLL;
+    for (int jb = a0; jb < a1; jb += 128) {
+        ChunkLoads c0 = load_chunk_a(lane, jb, a1, Acol, Aval);
+        ChunkLoads c1 = load_chunk_a(lane, jb + 64, a1, Acol, Aval);
+        load_chunk_meta(c0, bmeta);
+        load_chunk_meta(c1, bmeta);
+        const StagedChunk x0 = finish_chunk(lane, c0, tiles);
+        wave_chunk(x0, chunk_group(x0.nh, avg, U, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN), f);
+        if (jb + 64 < a1) {
+            const StagedChunk x1 = finish_chunk(lane, c1, tiles);
+            wave_chunk(x1, chunk_group(x1.nh, avg, U, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN), f);
+        }
+    }
+}
+
 template <class F>
 __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
                                              const int* __restrict__ Acol,
@@ -1122,51 +1186,73 @@ __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
 // j also holds the a-values of rows head+1 .. head+R-1 (rows of one pattern are
 // consecutive and equally long in A: entry j of row head+r sits at j + r*nA).
 template <class F>
+__device__ __forceinline__ void group_chunk(const StagedChunk& x, const double (&avr)[RG_MAX], int avg, const F& f,
+                                            int R, int stride) {
+    constexpr int RM = RG_MAX;
+    const int lane = lane_id();
+    // the chunk's own lane-group width (a row's short last chunk takes wide groups: one
+    // load batch for its few visits instead of the row's batches per visit)
+    const int G = chunk_group(x.nh, avg, MHS_GRP_UNROLL, x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
+    const int gs = 31 - __clz(G);
+    const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
+    const int iters = (x.nh + ngrp - 1) / ngrp;
+    for (int it = 0; it < iters; ++it) {
+        const int e = grp * iters + it;
+        const int h = __shfl(x.src, e & 63);
+        const int sb = __shfl(x.st, h);
+        const int n0 = __shfl(x.ln, h);
+        const int n = e < x.nh ? n0 : 0;
+        const int L = __shfl(x.L, h);
+        if (x.lmax == 1) {
+            double a[RM][1];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) a[r][0] = __shfl(avr[r], h);
+            run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
+        } else {
+            double a[RM][3];
+#pragma unroll
+            for (int r = 0; r < RM; ++r)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h + i, 63));
+            if (__ballot(n > 0 && L != 3) == 0)
+                run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
+            else
+                run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
+        }
+    }
+}
+
+// Row group (wave teams only): the head row's A entries are staged as usual and lane
+// j also holds the a-values of rows head+1 .. head+R-1 (rows of one pattern are
+// consecutive and equally long in A: entry j of row head+r sits at j + r*nA).  Chunks
+// are staged in pairs: both chunks' A loads and then both bmeta loads are issued before
+// the first is walked, so the second chunk's two dependent round trips overlap the
+// first chunk's sweeps (a 69-entry FEM row: 63 + 6 entries).
+template <class F>
 __device__ __forceinline__ void for_products_group(int a0, int a1, const int* __restrict__ Acol,
                                                    const double* __restrict__ Aval,
-                                                   const int4* __restrict__ bmeta, int Grow, const F& f,
+                                                   const int4* __restrict__ bmeta, int avg, const F& f,
                                                    int R, int nA, int stride) {
     constexpr int RM = RG_MAX;
     static_assert(MHS_RUN_MAX <= 3, "grouped walks merge runs of up to 3 B rows");
     const int lane = lane_id();
     // chunks of MHS_GRP_CHUNK entries: 63 keeps the 3-entry runs of dof-3 rows whole (a chunk
     // edge cuts a run: a 1-entry visit in one chunk, a 2-entry one in the next, masked sweeps)
-    for (int jb = a0; jb < a1; jb += MHS_GRP_CHUNK) {
-        const int ce = min(a1, jb + MHS_GRP_CHUNK);
-        const StagedChunk x = stage_chunk(lane, jb, ce, Acol, Aval, bmeta, false);
-        const int jl = jb + lane;
-        double avr[RM];
-        avr[0] = x.av;
+    for (int jb = a0; jb < a1; jb += 2 * MHS_GRP_CHUNK) {
+        const int ce0 = min(a1, jb + MHS_GRP_CHUNK), jb1 = ce0, ce1 = min(a1, jb1 + MHS_GRP_CHUNK);
+        ChunkLoads c0 = load_chunk_a(lane, jb, ce0, Acol, Aval);
+        double avr0[RM], avr1[RM];
+        avr0[0] = c0.av;
 #pragma unroll
-        for (int r = 1; r < RM; ++r) avr[r] = (jl < ce && r < R) ? Aval[jl + r * nA] : 0.0;
-        const int G = (x.lmax > 1 && Grow < MHS_RUN_GMIN) ? MHS_RUN_GMIN : Grow;
-        const int gs = 31 - __clz(G);
-        const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
-        const int iters = (x.nh + ngrp - 1) / ngrp;
-        for (int it = 0; it < iters; ++it) {
-            const int e = grp * iters + it;
-            const int h = __shfl(x.src, e & 63);
-            const int sb = __shfl(x.st, h);
-            const int n0 = __shfl(x.ln, h);
-            const int n = e < x.nh ? n0 : 0;
-            const int L = __shfl(x.L, h);
-            if (x.lmax == 1) {
-                double a[RM][1];
+        for (int r = 1; r < RM; ++r) avr0[r] = (jb + lane < ce0 && r < R) ? Aval[jb + lane + r * nA] : 0.0;
+        ChunkLoads c1 = load_chunk_a(lane, jb1, ce1, Acol, Aval);
+        avr1[0] = c1.av;
 #pragma unroll
-                for (int r = 0; r < RM; ++r) a[r][0] = __shfl(avr[r], h);
-                run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
-            } else {
-                double a[RM][3];
-#pragma unroll
-                for (int r = 0; r < RM; ++r)
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h + i, 63));
-                if (__ballot(n > 0 && L != 3) == 0)
-                    run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
-                else
-                    run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
-            }
-        }
+        for (int r = 1; r < RM; ++r) avr1[r] = (jb1 + lane < ce1 && r < R) ? Aval[jb1 + lane + r * nA] : 0.0;
+        load_chunk_meta(c0, bmeta);
+        load_chunk_meta(c1, bmeta);
+        group_chunk(finish_chunk(lane, c0, false), avr0, avg, f, R, stride);
+        if (jb1 < a1) group_chunk(finish_chunk(lane, c1, false), avr1, avg, f, R, stride);
     }
 }
 
@@ -1299,6 +1385,10 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
                                               const int4* __restrict__ bmeta, bool tiles,
                                               long long work, const F& f, int4* stage) {
     const int nA = a1 - a0;
+    if constexpr (Team::size == 64 && MHS_WAVE_PAIRS && F::kPairs) {
+        wave_walk(a0, a1, Acol, Aval, bmeta, tiles, work, f);
+        return;
+    }
     for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
                  pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN,
                             tiles ? 1 : (Team::size > 64 ? MHS_UNROLL_BLOCK : MHS_UNROLL)),  // (tile walks: by entries)
@@ -1312,6 +1402,7 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
 // Tables hold >= 2x the distinct tiles, so an insert always finds a slot.
 struct TileBuild {
     static constexpr bool kValues = false;
+    static constexpr bool kPairs = false;  // wave walks may stage chunk pairs (registers)
     TileEntry* E;
     bool direct;
     int lo, H;
@@ -1347,6 +1438,7 @@ struct TileBuild {
 template <bool GM, int MODE>
 struct Accum {
     static constexpr bool kValues = true;
+    static constexpr bool kPairs = MODE != NM_HASH;  // (the hash kernels run at 64 VGPRs: pairs spill)
     const TileEntry* E;
     double* acc;
     int lo, H, colbase;
@@ -1428,6 +1520,7 @@ static_assert(WIDE_WT * 9 <= B1024_BYTES, "a wide window fits the 1024-thread ke
 // Wide-row tile walk: OR each B tile inside the window [w0, w1) into a dense mask array.
 struct WideTiles {
     static constexpr bool kValues = false;
+    static constexpr bool kPairs = false;  // wave walks may stage chunk pairs (registers)
     unsigned long long* masks;
     int w0, w1;
     const int* __restrict__ btcol;
@@ -1457,6 +1550,7 @@ __device__ __forceinline__ int span_rank(const unsigned long long* bm, const int
 }
 struct SpanBits {
     static constexpr bool kValues = false;
+    static constexpr bool kPairs = false;  // wave walks may stage chunk pairs (registers)
     unsigned long long* bm;
     int lo;
     const int* __restrict__ btcol;
@@ -1472,6 +1566,7 @@ struct SpanBits {
 };
 struct RankedMasks {
     static constexpr bool kValues = false;
+    static constexpr bool kPairs = false;  // wave walks may stage chunk pairs (registers)
     const unsigned long long* bm;
     const int* wpre;
     unsigned long long* msk;
@@ -1555,6 +1650,7 @@ struct SymArgs {
 // 8 or 12 bytes a slot (sym_need), so more rows fit the small-table wave bin.
 struct SymTileBuild {
     static constexpr bool kValues = false;
+    static constexpr bool kPairs = true;  // wave walks may stage chunk pairs (registers)
     unsigned long long* Mk;
     int* Kk;
     bool direct;
@@ -2386,8 +2482,10 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     {
         const Accum<GLOBALMEM, MODE> f{E, acc, lo, H, colbase, a.Bcol, a.Bval};
         if constexpr (GROUPED) {
-            for_products_group(a0, a1, a.Acol, a.Aval, a.bmeta, pick_group(a.rflop[row], a1 - a0, 64), f, R,
-                               a1 - a0, stride);
+            const int nAr = a1 - a0;
+            for_products_group(a0, a1, a.Acol, a.Aval, a.bmeta,
+                               nAr > 0 ? (__builtin_amdgcn_readfirstlane(a.rflop[row]) + nAr - 1) / nAr : 1, f, R,
+                               nAr, stride);
         } else {
             walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
         }
@@ -2485,6 +2583,7 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
 
 struct WideAccum {
     static constexpr bool kValues = true;
+    static constexpr bool kPairs = false;  // wave walks may stage chunk pairs (registers)
     const unsigned long long* masks;
     const int* base4;
     int w0, w1;
@@ -2566,6 +2665,7 @@ __device__ void num_row_wide(const BlockTeam<T, false>& tm, const NumArgs& a, in
 template <bool GM>
 struct RankAccum {
     static constexpr bool kValues = true;
+    static constexpr bool kPairs = false;  // wave walks may stage chunk pairs (registers)
     const unsigned long long* bm;
     const int* wpre;
     const unsigned long long* msk;
