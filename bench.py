@@ -58,12 +58,12 @@ METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
 # mh-spgemm_amd/csrc/mhs_internal.hpp): numeric bins NUM_TINY + c, c = 0..5
 TINY_WK = [(4, 2), (8, 4), (16, 4), (32, 4), (64, 4), (64, 8)]
 # numeric bin id -> kernel (mhs_internal.hpp NumBin; include/mhspgemm.h num_bins)
-NUM_BIN_KERNELS = (["", "k_num_wave_direct<5120>", "k_num_wave_direct<16384>", "k_num_block<256>",
+NUM_BIN_KERNELS = (["", "k_num_wave_direct<5120>", "k_num_wave_direct<10240>", "k_num_block<256>",
                     "k_num_block<1024>", "k_num_block<1024,global>", "k_num_wave<10240,grouped>",
-                    "k_num_wave<16384,grouped>"]
+                    "k_num_wave<10240,grouped> (up to 32 K products)"]
                    + [f"k_tiny_num_small({w}x{k}) (numeric-first rows: k_tiny_copy_rows)" if w <= 32
                       else f"k_tiny_num<{w},{k}>" for w, k in TINY_WK]
-                   + ["k_num_wave_hash<5120>", "k_num_wave_hash<16384>"])
+                   + ["k_num_wave_hash<5120>", "k_num_wave_hash<10240>"])
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 

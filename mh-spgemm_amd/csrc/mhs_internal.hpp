@@ -110,7 +110,10 @@ constexpr int SYM_B256_BYTES = 32768;
 constexpr int SYM_B256_WORK = 1 << 20;
 constexpr int NUM_WS_BYTES = 5120;     // 4 waves x 5 KiB = 20 KiB/block: 8 blocks (32 waves) per CU
 constexpr int NUM_WS_WORK = 8192;       // products a single wave takes on
-constexpr int NUM_W16_BYTES = 16384;
+// The bigger wave bins: 10 KiB a wave, 4 blocks (16 waves) per CU (round 3: 16 KiB left 2
+// blocks per CU; rows past 10 KiB now take the 256-thread block bin -- cage15-like -3 %,
+// cant-s1-like -4 %, pdb1HYS-like -4 %, wb-edu-like -3..9 %, others neutral: profiles/r03)
+constexpr int NUM_W16_BYTES = 10240;
 constexpr int NUM_W16_WORK = 32768;
 constexpr int NUM_WSG_BYTES = 10240;   // grouped rows: 4 waves x 10 KiB = 40 KiB/block (4 per CU)
 constexpr int NUM_B256_BYTES = 65536;

@@ -55,7 +55,7 @@
 #define MHS_TINY64_GRID 4096  // block cap of the 64-lane tiny numeric launches (8192: wb-edu-like +6 %)
 #endif
 #ifndef MHS_NUM_W16H_GRID
-#define MHS_NUM_W16H_GRID 2048  // block cap of the 16 KiB hash launch (4096: neutral, profiles/r02za2_grid)
+#define MHS_NUM_W16H_GRID 2048  // block cap of the 10 KiB hash launch (4096: neutral at 16 KiB, profiles/r02za2_grid)
 #endif
 #ifndef MHS_NUM_WSX_GRID
 #define MHS_NUM_WSX_GRID 16384  // ... of the small-row hash / direct launches (8192: cage15-like numeric +4.5 %, 4096: +13 %,
@@ -389,7 +389,7 @@ static_assert(MHS_GRP_CHUNK >= 1 && MHS_GRP_CHUNK <= 64, "a chunk is one entry p
 #define MHS_SYMWM_DYN_MAX 32768  // k_sym_rare's 10 KiB wave rows from the cursors up to this many rows
 #endif
 #ifndef MHS_DYN16_MAX
-#define MHS_DYN16_MAX 32768  // hash 16 KiB bins of at most this many rows: all rows from the cursor
+#define MHS_DYN16_MAX 32768  // hash 10 KiB bins of at most this many rows: all rows from the cursor
 #endif
 #ifndef MHS_GUIDED_STATIC
 #define MHS_GUIDED_STATIC 4  // eighths of an XCD group's rows walked statically before the cursor
@@ -2804,7 +2804,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
             num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH>(tm, a, row, reg + WAVE_HDR,
                                                                              (int*)reg, nullptr);
     };
-    // The 16 KiB bins hold the heaviest wave rows (power-law rows of hundreds of tiles, a
+    // The 10 KiB bins (16 KiB before round 3) hold the heaviest wave rows (power-law rows of hundreds of tiles, a
     // few rows per wave): a static stride leaves the launch's end to the wave that drew the
     // heaviest ones.  Guided walk: each XCD group's waves stride statically through the first
     // MHS_GUIDED_STATIC/8 of its eighth of the list (row locality, no atomics), then take the
