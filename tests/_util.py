@@ -89,8 +89,10 @@ def bin_zoo(seed: int = 11):
             arows.append(sorted(rng.choice(np.arange(1000, K - 1), nb, replace=False).tolist()))
     for i in range(4):                               # > 512 products, 50 tiles: hash, wave
         arows.append([int(rng.integers(1000, K - 1))] * 12)
-    for i in range(4):                               # > 512 products, ~300 tiles: hash, 16 KiB wave
+    for i in range(4):                               # > 512 products, ~300 tiles: hash, 256-thread block
         arows.append(sorted(rng.choice(np.arange(1000, K - 1), 6, replace=False).tolist() * 2))
+    for i in range(4):                               # > 512 products, ~200 tiles: hash, 10 KiB wave
+        arows.append(sorted(rng.choice(np.arange(1000, K - 1), 4, replace=False).tolist() * 3))
     for i in range(6):                               # scattered medium: hash, 256-thread block
         arows.append(sorted(rng.choice(np.arange(1000, K - 1), 20, replace=False).tolist()))
     for i in range(4):                               # scattered large: 1024-thread block
