@@ -1158,6 +1158,8 @@ __device__ __forceinline__ void wave_walk(int a0, int a1, const int* __restrict_
     const int lane = lane_id();
     const int nA = a1 - a0;
     const int avg = nA > 0 ? (int)((work + nA - 1) / nA) : 1;
+    // (tile walks pick by entries, U = 1: picking by their 2-entry batches made the groups
+    // narrower, more visits at once, more same-address LDS atomics -- cage15-like symbolic +8 %)
     const int U = tiles ? 1 : MHS_UNROLL;
     for (int jb = a0; jb < a1; jb += 128) {
         ChunkLoads c0 = load_chunk_a(lane, jb, a1, Acol, Aval);
@@ -1185,10 +1187,11 @@ __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
 // Row group (wave teams only): the head row's A entries are staged as usual and lane
 // j also holds the a-values of rows head+1 .. head+R-1 (rows of one pattern are
 // consecutive and equally long in A: entry j of row head+r sits at j + r*nA).
-template <class F>
-__device__ __forceinline__ void group_chunk(const StagedChunk& x, const double (&avr)[RG_MAX], int avg, const F& f,
-                                            int R, int stride) {
+template <int RC, class F>
+__device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double (&avr)[RG_MAX], int avg, const F& f,
+                                              int Rrt, int stride) {
     constexpr int RM = RG_MAX;
+    const int R = RC ? RC : Rrt;  // RC: the group size as a constant (no per-row branches in the adds)
     const int lane = lane_id();
     // the chunk's own lane-group width (a row's short last chunk takes wide groups: one
     // load batch for its few visits instead of the row's batches per visit)
@@ -1220,6 +1223,15 @@ __device__ __forceinline__ void group_chunk(const StagedChunk& x, const double (
                 run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
         }
     }
+}
+template <class F>
+__device__ __forceinline__ void group_chunk(const StagedChunk& x, const double (&avr)[RG_MAX], int avg, const F& f,
+                                            int R, int stride) {
+    if (R == RG_MAX) {  // full groups (FEM dof triples): no per-row branches (cant-like numeric -3 %)
+        group_chunk_r<RG_MAX>(x, avr, avg, f, R, stride);
+        return;
+    }
+    group_chunk_r<0>(x, avr, avg, f, R, stride);
 }
 
 // Row group (wave teams only): the head row's A entries are staged as usual and lane
@@ -2332,6 +2344,8 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
     const bool rank_bitmap = MODE == NM_HASH && (Team::size > 64 || t >= 64) &&
                              (long long)((span + 63) >> 6) * 12 + 16 + (long long)t * 4 <=
                                  num_acc_bytes(NM_HASH, span, t, n);
+    // (a two-level bitmap over the span -- O(H) LDS work where counting costs t^2/64 -- measured
+    // cage15-like numeric +3 %: more dependent LDS steps per row; the kernel is latency-bound)
     const bool rank_count = MODE == NM_HASH && !rank_bitmap &&
                             (t <= HASH_CNT_T || (long long)((t + Team::size - 1) / Team::size) * t <= 768);
     bool have_list = false;  // the count list is already in acc
