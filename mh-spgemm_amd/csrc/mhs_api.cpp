@@ -41,6 +41,7 @@ struct mhs_ctx {
     hipEvent_t ev[8] = {};
     bool sync = true;      // MHS_OPT_SYNC
     bool groups = true;     // row groups (MHS_NO_GROUPS=1: every row alone)
+    bool near = true;       // near row groups (GRP_NEAR; MHS_NO_NEAR=1: off)
     // MHS_OPT_NUMERIC_EVENTS: ring of (start, end) events around the numeric phase
     std::vector<hipEvent_t> nev;
     long long ncalls = 0;
@@ -70,6 +71,17 @@ struct mhs_ctx {
     int num_streams = 4;
     hipStream_t aux[NAUX] = {};
     hipEvent_t fork_ev = nullptr, join_ev[NAUX] = {};
+    // launch-ahead numeric (SpecPlan, MHS_OPT_LAUNCH_AHEAD): the operands and Stats of the
+    // last call that ran the whole matrix; a call on the same operands queues that call's
+    // numeric launches behind k_scan instead of waiting for its own Stats first
+    bool launch_ahead = true;
+    struct Plan {
+        bool valid = false;
+        int AM = 0, AN = 0, Annz = 0, BM = 0, BN = 0, Bnnz = 0;
+        const void* arrays[4] = {};
+        Stats h{};
+    } plan;
+    long long ahead_hits = 0, ahead_misses = 0;
 };
 
 namespace {
@@ -165,11 +177,12 @@ void pool_put(mhs_ctx* ctx, void* p) {
 
 struct Layout {
     size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, asame, grp, bin_list, scan_part, mcache,
-        stats, blkflop, spill_mask, spill_key, lofs, tslot, nft_bin, total;
+        stats, spec, blkflop, spill_mask, spill_key, lofs, tslot, nft_bin, near_list, ucol, uval, gna, total;
+    bool near;
     long long spill_cap;
 };
 
-Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_total = -1) {
+Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_total = -1, bool near = false) {
     Layout L{};
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -179,6 +192,7 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     };
     const size_t nscan = (size_t)(M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1;
     L.stats = take(sizeof(Stats));
+    L.spec = take(SPEC_INTS * 4);
     L.btcol = take((size_t)nnzB * 4);
     L.btmask = take((size_t)nnzB * 8);
     L.bmeta = take((size_t)MB * 16);
@@ -205,6 +219,13 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     L.lofs = take((size_t)M * 4);
     L.tslot = take((size_t)M * 8);
     L.nft_bin = take((size_t)M);
+    L.near = near;
+    if (near) {  // near row groups: candidate list, union rows (see Work)
+        L.near_list = take((size_t)M * 4);
+        L.ucol = take((size_t)nnzA * 4);
+        L.uval = take((size_t)nnzA * 24);
+        L.gna = take((size_t)M * 4);
+    }
     L.total = o;
     return L;
 }
@@ -273,7 +294,14 @@ Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, int Bn, int
     w.spill.top = w.cursors + SPILL_CURSOR_SLOT * 8 * CURSOR_STRIDE;  // zeroed with the cursors
     w.spill.cap = L.spill_cap;
     w.tslot = (long long*)(ctx->ws + L.tslot);
+    if (L.near) {
+        w.near_list = (int*)(ctx->ws + L.near_list);
+        w.ucol = (int*)(ctx->ws + L.ucol);
+        w.uval = (double*)(ctx->ws + L.uval);
+        w.gna = (int*)(ctx->ws + L.gna);
+    }
     w.stats = (Stats*)(ctx->ws + L.stats);
+    w.spec = (int*)(ctx->ws + L.spec);
     w.gscratch = ctx->gscratch;
     w.gscratch_bytes = ctx->gscratch_bytes;
     return w;
@@ -313,6 +341,51 @@ int front_pass(mhs_ctx* ctx, const Csr& a, const Csr& b, Work& w, int* Cptr, boo
 int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h);
 
 constexpr int NUM_GLOBAL_GRID = 128;
+
+// The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
+// the aux streams, which join the call's stream again; spec: launch-ahead (SpecPlan).
+int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out,
+                const int* spec) {
+    hipStream_t s = ctx->stream;
+    // several heavy bins: deal them over the aux streams (fork/join costs ~10-20 us,
+    // so only when there are at least 3 launches of a product worth it)
+    hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
+    const int nl = numeric_launches(h);
+    const int nss = (nl >= 3 && h.flop >= (1ull << 24)) ? std::min(ctx->num_streams, nl) : 1;
+    if (nss > 1) {
+        MHS_HIP(hipEventRecord(ctx->fork_ev, s));
+        for (int i = 1; i < nss; ++i) {
+            ss[i] = ctx->aux[i - 1];
+            MHS_HIP(hipStreamWaitEvent(ss[i], ctx->fork_ev, 0));
+        }
+    }
+    const int used =
+        launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID, ctx->dense_span_max, spec);
+    MHS_HIP(hipGetLastError());
+    for (int i = 1; i < nss; ++i)
+        if (used & (1 << i)) {
+            MHS_HIP(hipEventRecord(ctx->join_ev[i - 1], ss[i]));
+            MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[i - 1], 0));
+        }
+    return MHS_OK;
+}
+
+// Launch-ahead applies: same operands as the plan's call, whose numeric pass had no global
+// bin (its scratch is sized from the Stats) and a non-empty C.
+bool plan_matches(const mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B) {
+    const auto& p = ctx->plan;
+    return p.valid && p.AM == A->M && p.AN == A->N && p.Annz == A->nnz && p.BM == B->M && p.BN == B->N &&
+           p.Bnnz == B->nnz && p.arrays[0] == A->ptr && p.arrays[1] == A->col && p.arrays[2] == B->ptr &&
+           p.arrays[3] == B->col && p.h.nnzC > 0 && p.h.num_count[NUM_GLOBAL] == 0;
+}
+
+void keep_plan(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, const Stats& h) {
+    auto& p = ctx->plan;
+    p.valid = true;
+    p.AM = A->M, p.AN = A->N, p.Annz = A->nnz, p.BM = B->M, p.BN = B->N, p.Bnnz = B->nnz;
+    p.arrays[0] = A->ptr, p.arrays[1] = A->col, p.arrays[2] = B->ptr, p.arrays[3] = B->col;
+    p.h = h;
+}
 
 int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h) {
     if (h.num_count[NUM_GLOBAL] <= 0) return MHS_OK;
@@ -511,11 +584,13 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (getenv("MHS_NO_MCACHE")) ctx->use_mcache = false;
     if (const char* e = getenv("MHS_MC_LIST")) ctx->mc_list = atoi(e) < MC_LIST_MIN ? MC_LIST_MIN : atoi(e);
     if (getenv("MHS_NO_GROUPS")) ctx->groups = false;
+    if (getenv("MHS_NO_NEAR")) ctx->near = false;
     if (getenv("MHS_NO_TINY_NUM")) ctx->tiny_num = false;
     if (const char* e = getenv("MHS_NFT_MIN_M")) ctx->nft_min_m = atoll(e);
     if (getenv("MHS_NFT_NO_SLOTS")) ctx->nft_slots = false;
     if (const char* e = getenv("MHS_SYM_FORK")) ctx->sym_fork = atoi(e) != 0;
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
+    if (const char* e = getenv("MHS_LAUNCH_AHEAD")) ctx->launch_ahead = atoi(e) != 0;
     *out = ctx;
     return MHS_OK;
 }
@@ -618,7 +693,11 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
 
     // ---- mem_alloc: workspace (cached across calls) + C.ptr --------------------
     const int mc_list = ctx->mc_list > 0 ? ctx->mc_list : mc_list_for(M);
-    const Layout L = plan(M, MB, A->nnz, B->nnz, mc_list);
+    const bool probe = ctx->tiny_num && ctx->nft_min_m >= 0 && M >= ctx->nft_min_m && M > 0;
+    // near row groups: with the row cache (their C patterns are compared there), not with
+    // the numeric-first probe (big M), and union rows of at most 3 x 32 M values
+    const bool near = ctx->near && ctx->groups && ctx->use_mcache && !probe && A->nnz <= (1 << 25);
+    const Layout L = plan(M, MB, A->nnz, B->nnz, mc_list, -1, near);
     const char* ws_before = ctx->ws;
     int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
     if (rc == MHS_ERR_OOM && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
@@ -651,7 +730,6 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // ---- symbolic_binning ---------------------------------------------------------
     // numeric-first tiny rows (big M): k_analyze also bins the rows that way and counts
     // them; the host picks the bin lists and sizes the candidates' value slots
-    const bool probe = w.tiny_num && ctx->nft_min_m >= 0 && M >= ctx->nft_min_m && M > 0;
     unsigned long long other = 0;
     if (probe) w.nft_bin = (unsigned char*)(ctx->ws + L.nft_bin);
     const int seq_probe = probe ? ++ctx->seq : 0;
@@ -694,24 +772,57 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         launch_symbolic_common(a, b, w, M, N, out.ptr, s);
         launch_symbolic_rare(a, w, M, N, out.ptr, s);
     }
+    launch_near(a, w, out.ptr, s);
     MHS_HIP(hipGetLastError());
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
     Stats h;
+    const int nring = (int)ctx->nev.size() / 2;
+    const int slot = nring ? (int)(ctx->ncalls % nring) : 0;
+    bool ahead = false;  // launch-ahead numeric queued (SpecPlan)
     if (M > 0) {
+        // launch-ahead: the same operands as the last call's -- queue its numeric launches
+        // (C of its size) behind k_scan, which checks that they fit this call's bins
+        SpecPlan sp{};
+        if (ctx->launch_ahead && !timed && !probe && plan_matches(ctx, A, B)) {
+            if (alloc_c(ctx, &out, ctx->plan.h.nnzC) == hipSuccess) {
+                ahead = true;
+                numeric_spec_plan(ctx->plan.h, sp);
+                sp.out = w.spec;
+                sp.cap = ctx->plan.h.nnzC;
+            } else {
+                (void)hipGetLastError();
+                out.col = nullptr;
+                out.val = nullptr;
+            }
+        }
         // the numeric bin offsets kernel publishes Stats to pinned host memory; the
         // host spins on the sequence number (no stream sync, no interrupt wake-up)
         const int seq = ++ctx->seq;
-        launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
+        launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq, sp);
         MHS_HIP(hipGetLastError());
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
-        rc = wait_published(ctx, s, ctx->pub, seq);
+        if (ahead) {
+            if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
+            rc = run_numeric(ctx, a, b, w, ctx->plan.h, out, w.spec);
+        }
+        if (!rc) rc = wait_published(ctx, s, ctx->pub, seq);
         if (rc) {
-            pool_put(ctx, out.ptr);
+            mhs_ctx_recycle(ctx, &out);
             return rc;
         }
         memcpy(&h, (const void*)&ctx->pub->stats, sizeof(Stats));
         ctx->stats_zero = true;  // k_scan's last block cleared them after publishing
+        if (ahead && !h.spec_ok) {  // the plan did not fit: those launches returned at once
+            pool_put(ctx, out.col);
+            pool_put(ctx, out.val);
+            out.col = nullptr;
+            out.val = nullptr;
+            ahead = false;
+            ++ctx->ahead_misses;
+        } else if (ahead) {
+            ++ctx->ahead_hits;
+        }
     } else {
         MHS_HIP(hipGetLastError());
         MHS_HIP(hipMemcpyAsync(ctx->h_stats, w.stats, sizeof(Stats), hipMemcpyDeviceToHost, s));
@@ -730,9 +841,11 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     }
     out.nnz = (int)h.nnzC;
 
+    if (M > 0 && !probe) keep_plan(ctx, A, B, h);
+
     // ---- Malloc_C_col_val ---------------------------------------------------------------
     const auto T5 = std::chrono::steady_clock::now();
-    {
+    if (!ahead) {
         const hipError_t e = alloc_c(ctx, &out, out.nnz);
         if (e != hipSuccess) {
             pool_put(ctx, out.ptr);
@@ -742,7 +855,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
             return fail_hip(ctx, e, "allocating C.col/C.val");
         }
     }
-    rc = ensure_gscratch(ctx, w, h);
+    rc = ahead ? MHS_OK : ensure_gscratch(ctx, w, h);
     if (rc) {
         mhs_ctx_recycle(ctx, &out);
         (void)hipGetLastError();
@@ -753,30 +866,15 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
 
     // ---- Numeric -------------------------------------------------------------------------
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
-    const int nring = (int)ctx->nev.size() / 2;
-    const int slot = nring ? (int)(ctx->ncalls % nring) : 0;
-    if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
-    if (out.nnz > 0) {
-        // several heavy bins: deal them over the aux streams (fork/join costs ~10-20 us,
-        // so only when there are at least 3 launches of a product worth it)
-        hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
-        const int nl = numeric_launches(h);
-        int nss = (nl >= 3 && h.flop >= (1ull << 24)) ? std::min(ctx->num_streams, nl) : 1;
-        if (nss > 1) {
-            MHS_HIP(hipEventRecord(ctx->fork_ev, s));
-            for (int i = 1; i < nss; ++i) {
-                ss[i] = ctx->aux[i - 1];
-                MHS_HIP(hipStreamWaitEvent(ss[i], ctx->fork_ev, 0));
+    if (!ahead) {
+        if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
+        if (out.nnz > 0) {
+            rc = run_numeric(ctx, a, b, w, h, out, nullptr);
+            if (rc) {
+                mhs_ctx_recycle(ctx, &out);
+                return rc;
             }
         }
-        const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
-                                        ctx->dense_span_max);
-        MHS_HIP(hipGetLastError());
-        for (int i = 1; i < nss; ++i)
-            if (used & (1 << i)) {
-                MHS_HIP(hipEventRecord(ctx->join_ev[i - 1], ss[i]));
-                MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[i - 1], 0));
-            }
     }
     MHS_HIP(hipGetLastError());
     if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
@@ -868,12 +966,19 @@ int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
     case MHS_OPT_TINY_FIRST_ROWS:
         ctx->nft_min_m = value;
         return MHS_OK;
+    case MHS_OPT_LAUNCH_AHEAD:
+        ctx->launch_ahead = value != 0;
+        return MHS_OK;
     default:
         return fail(ctx, MHS_ERR_INVALID, "unknown option");
     }
 }
 
 long long mhs_ctx_chunked_calls(const mhs_ctx* ctx) { return ctx ? ctx->chunked_calls : -1; }
+
+long long mhs_ctx_launch_ahead_calls(const mhs_ctx* ctx, int misses) {
+    return ctx ? (misses ? ctx->ahead_misses : ctx->ahead_hits) : -1;
+}
 
 int mhs_ctx_numeric_ms(mhs_ctx* ctx, float* out, int n) {
     if (!ctx || (!out && n > 0)) return -MHS_ERR_INVALID;

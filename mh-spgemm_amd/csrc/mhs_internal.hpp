@@ -101,6 +101,16 @@ enum NumBin : int {
 constexpr int RG_MAX = 3;
 constexpr int RG_BREAK = 96;  // a multiple of 2, 3, 4 and 6: dof blocks of those sizes stay whole
 constexpr int GRP_CONT = 0x80;
+// Near row groups: consecutive rows whose A patterns differ by a few entries (k_bin_list's
+// candidates: same C tile span, A lengths within NEAR_DLEN, same first or last column) and
+// whose C patterns turn out equal (k_near, after the symbolic pass counted each row on its
+// own).  Their numeric runs as a row group over the union of their A rows (ucol / uval:
+// columns once, R values each, 0 where a row lacks the column).  Head: R | GRP_NEAR.
+constexpr int GRP_NEAR = 0x40;
+constexpr int GRP_RMASK = 0x3F;
+constexpr int NEAR_DLEN = 16;
+constexpr int NEAR_WORDS = 256;   // union rows: A columns within a window of NEAR_WORDS * 64
+constexpr int NEAR_UMAX = 128;    // ... and at most this many union entries
 
 // Per-team LDS budgets (bytes).  The wave kernels carve one region per wave.
 constexpr int SYM_WAVE_BYTES = 5120;   // 4 waves x 5 KiB: 8 blocks (32 waves, the CU's cap) per CU
@@ -146,6 +156,8 @@ struct Stats {
     unsigned long long an_slots;   // numeric-first probe: the candidates' slot entries,
     unsigned long long an_other;   // rows with products past the tiny classes,
     int an_done;                   // and k_probe_publish blocks finished
+    int spec_ok;                   // the launch-ahead numeric ran this call's bins (SpecPlan)
+    int near_heads;                // near-group candidates listed by k_bin_list (k_near's work)
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
 // kernel writes it and then `seq`, the host spins on `seq` instead of a stream sync.
@@ -154,6 +166,20 @@ struct Published {
     int seq;
     int pad[3];
 };
+// Launch-ahead numeric (mhs_api.cpp): a call whose operands match the previous call's
+// queues that call's numeric launches right behind k_scan, before the host has this call's
+// Stats.  k_scan's last block checks that this call's bins fit those launches -- C capacity,
+// launched bins, the block kernels' LDS, no global bin, no input error -- and hands the
+// counts over: out[0] = fits, out[1 + b] = bin b's count.  The numeric kernels take their
+// counts from `out` and return at once when it does not fit (the host then launches for
+// the true counts).  Grids are persistent walks, so any count runs on any grid.
+struct SpecPlan {
+    int* out;       // nullptr: no launch-ahead this call
+    long long cap;  // C entries allocated
+    int mask;       // bins launched (bit b)
+    int lds[2];     // dynamic LDS of the NUM_B256 / NUM_B1024 launches
+};
+constexpr int SPEC_INTS = 1 + NBINS;
 constexpr int SAME_PATTERN = 0x40000000;  // bmeta.z flag: B row repeats row-1's columns
 constexpr int ERR_UNSORTED = 1;
 constexpr int ERR_COL_RANGE = 2;
@@ -329,6 +355,13 @@ struct Work {
     unsigned char* asame;    // M: row has the column pattern of row-1 (k_analyze)
     unsigned char* grp;      // M: row groups (k_bin_list; see RG_MAX)
     int groups;              // form row groups (0: every row alone)
+    // near row groups (GRP_NEAR; nullptr: off): candidate list (head * 4 + R), union rows
+    // at the head's A offset (ucol: nnz(A) ints; uval: 3 nnz(A) doubles, values of row r at
+    // 3 * Aptr[head] + r * nU), union length per head
+    int* near_list;
+    int* ucol;
+    double* uval;
+    int* gna;
     int tiny_num;            // numeric tiny classes allowed (per row: column span <= TINY_NUM_NMAX + 1)
     // numeric-first tiny rows (big M): the symbolic tiny launch sorts them once, in the
     // numeric classes, and sums their values into slots (sc_*); numeric only copies them
@@ -348,6 +381,7 @@ struct Work {
     int mc_list;                  // list cap (see mlisted)
     SpillArea spill;              // tile lists of rows past mc_list (symbolic -> numeric)
     Stats* stats;
+    int* spec;         // SPEC_INTS: launch-ahead verdict and counts (k_scan -> numeric)
     void* gscratch;    // global-bin scratch
     size_t gscratch_bytes;
 };
@@ -363,10 +397,16 @@ int analyze_blocks(long long nnzA, int M);
 
 void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s);
 void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s);
+// near row groups: verify k_bin_list's candidates after the symbolic pass, build union rows
+void launch_near(const Csr& A, const Work& w, const int* Cptr, hipStream_t s);
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
-                          Published* pub, int seq);
+                          Published* pub, int seq, const SpecPlan& sp = SpecPlan{});
+// spec != nullptr: launch-ahead (counts from spec; see SpecPlan), grids and LDS from h
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
-                   int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max);
+                   int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max,
+                   const int* spec = nullptr);
+// the bins and block-kernel LDS launch_numeric launches for h (launch-ahead: k_scan checks against them)
+void numeric_spec_plan(const Stats& h, SpecPlan& sp);
 // numeric launches a call makes for these bin counts (the 32-lane tiny classes share one)
 int numeric_launches(const Stats& h);
 size_t sym_global_bytes_per_block(int N);

@@ -89,6 +89,9 @@
 #ifndef MHS_SYM_B256_GRID
 #define MHS_SYM_B256_GRID 1024  // block cap of the persistent 256-thread symbolic bin launch
 #endif
+#ifndef MHS_WPE_HASH16
+#define MHS_WPE_HASH16 MHS_WPE_HASH  // the 10 KiB hash bin (LDS: 4 blocks = 4 waves per SIMD)
+#endif
 #ifndef MHS_WPE_GRP
 #define MHS_WPE_GRP 0  // occupancy floor of the generic / grouped wave numeric kernel (0: compiler's choice)
 #endif
@@ -140,6 +143,11 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
     return v;
 }
 
@@ -2047,38 +2055,211 @@ __global__ __launch_bounds__(1024) void k_probe_publish(const unsigned long long
     if (last_block_done(&stats->an_done)) publish_stats(stats, pub, seq);
 }
 
+// Near-group candidates (k_bin_list): the A rows the link test reads
+struct NearCand {
+    const int* Aptr;
+    const int* Acol;
+    const int* rlo;
+    const int* rhi;
+    int* list;  // nullptr: no near groups
+};
+
 template <int PER>
 __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* __restrict__ bin_id,
                                                    const unsigned char* __restrict__ asame,
                                                    unsigned char* __restrict__ grp, int groups,
                                                    int* __restrict__ list, const unsigned char* __restrict__ nft_bin,
-                                                   Stats* __restrict__ stats) {
+                                                   Stats* __restrict__ stats, NearCand nc) {
     __shared__ unsigned char binof[1024 * PER];
+    const int lane = lane_id();
+    // link of row r to row r-1: 1 = the same A pattern, 2 = a near candidate (see GRP_NEAR), 0 = none
+    auto link = [&](long long r) -> int {
+        if (asame[r]) return 1;
+        if (!nc.list || r == 0) return 0;
+        const int b0 = bin_id[r], b1 = bin_id[r - 1];
+        const bool t0 = b0 == SYM_NONE || (b0 >= SYM_TINY && b0 < SYM_TINY + TINY_NC);
+        const bool t1 = b1 == SYM_NONE || (b1 >= SYM_TINY && b1 < SYM_TINY + TINY_NC);
+        if (t0 || t1 || nc.rlo[r] != nc.rlo[r - 1] || nc.rhi[r] != nc.rhi[r - 1]) return 0;
+        const int s0 = nc.Aptr[r - 1], s1 = nc.Aptr[r], s2 = nc.Aptr[r + 1];
+        const int l0 = s1 - s0, l1 = s2 - s1;
+        if (l0 < 8 || l1 < 8 || l1 - l0 > NEAR_DLEN || l0 - l1 > NEAR_DLEN) return 0;
+        return (nc.Acol[s0] == nc.Acol[s1] || nc.Acol[s1 - 1] == nc.Acol[s2 - 1]) ? 2 : 0;
+    };
     for (int j = threadIdx.x; j < 1024 * PER; j += 1024) {
         const long long i = (long long)blockIdx.x * (1024 * PER) + j;
         unsigned char b = 0;
+        bool cand = false;  // head of a near candidate group (listed for k_near)
+        int cR = 0;
         if (i < M) {
             int g = 1;
             // a run of same-pattern rows is tiny throughout or not at all
             const int bi = nft_bin ? nft_bin[i] : bin_id[i];
             const bool solo = nft_bin && bi >= SYM_TINY && bi < SYM_TINY + TINY_SYM_NC;
-            if (groups && !solo && asame[i]) {
-                long long rs = i;
-                const long long lim = i - i % RG_BREAK;
-                while (rs > lim && asame[rs]) --rs;
-                const int o = (int)((i - rs) % RG_MAX);
-                if (o) g = GRP_CONT | o;
-            }
-            if (groups && !solo && g == 1) {  // a head: count the rows that follow it in its group
-                while (g < RG_MAX && i + g < M && (i + g) % RG_BREAK != 0 && asame[i + g]) ++g;
+            if (groups && !solo) {
+                // the run of linked rows through i is cut into groups of RG_MAX from its start
+                long long h = i;
+                if (link(i)) {
+                    long long rs = i;
+                    const long long lim = i - i % RG_BREAK;
+                    while (rs > lim && link(rs)) --rs;
+                    h = i - (i - rs) % RG_MAX;
+                }
+                int R = 1;
+                bool nearg = false;
+                while (R < RG_MAX && h + R < M && (h + R) % RG_BREAK != 0) {
+                    const int lk = link(h + R);
+                    if (!lk) break;
+                    nearg = nearg || lk == 2;
+                    ++R;
+                }
+                // near candidates: every row counted on its own by symbolic; k_near decides
+                if (!nearg) g = i == h ? R : (GRP_CONT | (int)(i - h));
+                cand = nearg && i == h;
+                cR = R;
             }
             grp[i] = (unsigned char)g;
             b = (g & GRP_CONT) ? 0 : bi;
+        }
+        const unsigned long long bal = __ballot(cand);
+        if (bal) {  // one counter add per wave
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&stats->near_heads, __popcll(bal));
+            base = __shfl(base, 0);
+            if (cand) nc.list[base + __popcll(bal & lanemask_lt())] = (int)(i * 4 + cR);
         }
         binof[j] = b;
     }
     __syncthreads();
     append_block_rows<SYM_NB, PER>(binof, M, stats->sym_count, list, (int)blockIdx.x);
+}
+
+// Near groups (k_bin_list's candidate list), one wave per candidate after the symbolic
+// pass: the rows' C patterns must be equal -- counts, tile spans, and the row cache's tile
+// masks (direct-mapped tables only: their lists come out in tile order) -- else the rows
+// stay alone.  A verified group gets its union row: the rows' A columns marked in a bitmap
+// over their column window, ranked by prefix popcounts; R value slices (0 where a row lacks
+// the column) staged in LDS and copied out.  Then grp marks it (head R | GRP_NEAR).
+struct NearArgs {
+    const int* Aptr;
+    const int* Acol;
+    const double* Aval;
+    const int* Cptr;  // the symbolic counts (before the scan)
+    const int* ctiles;
+    const int* rlo;
+    const int* rhi;
+    const int* rflop;
+    const int* rtflop;
+    const unsigned long long* mcache;
+    int mc_list, mc_stride;
+    const int* list;
+    const Stats* stats;
+    unsigned char* grp;
+    int* ucol;
+    double* uval;
+    int* gna;
+};
+#ifndef MHS_NEAR_GRID
+#define MHS_NEAR_GRID 2048  // k_near's block cap
+#endif
+constexpr int NEAR_PER = 4;  // A entries a lane holds: a group's R rows of at most 256 entries
+__global__ __launch_bounds__(256) void k_near(NearArgs p) {
+    __shared__ unsigned long long bm_s[WPB][NEAR_WORDS];
+    __shared__ int wpre_s[WPB][NEAR_WORDS];
+    __shared__ double uv_s[WPB][RG_MAX * NEAR_UMAX];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    unsigned long long* bm = bm_s[w];
+    int* wpre = wpre_s[w];
+    double* uv = uv_s[w];
+    const WaveTeam tm;
+    const int count = __hip_atomic_load(&p.stats->near_heads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every step's loads are independent of each other: three round trips per group
+    for (int li = (int)blockIdx.x * WPB + w; li < count; li += (int)gridDim.x * WPB) {
+        const int e = __builtin_amdgcn_readfirstlane(p.list[li]);
+        const int h = e >> 2, R = e & 3;
+        // 1. the rows' scalars, lane r for row h + r
+        const bool rl = lane < R;
+        int n = 0, t = 0, tf = 0, fl = 0, a0 = 0, a1 = 0;
+        if (rl) {
+            n = p.Cptr[h + lane];
+            t = p.ctiles[h + lane];
+            tf = p.rtflop[h + lane];
+            fl = p.rflop[h + lane];
+            a0 = p.Aptr[h + lane];
+            a1 = p.Aptr[h + lane + 1];
+        }
+        const int lo = __builtin_amdgcn_readfirstlane(p.rlo[h]);
+        const int span = __builtin_amdgcn_readfirstlane(p.rhi[h]) - lo + 1;
+        // the row cache form of each row's C pattern (1: masks over the span, 2: a tile list)
+        const int f = !rl || !sym_direct(span, tf) || tiny_class_sym(fl, a1 - a0) >= 0 ? 0
+                      : mcached(span, tf)                                              ? 1
+                      : mlisted(span, tf, t, p.mc_list)                                ? 2
+                                                                                       : 0;
+        const int n0 = __builtin_amdgcn_readfirstlane(n), t0 = __builtin_amdgcn_readfirstlane(t);
+        const int f0 = __builtin_amdgcn_readfirstlane(f);
+        const int A0 = __builtin_amdgcn_readfirstlane(a0), A1 = __shfl(a1, R - 1);
+        const int b1 = __shfl(a0, 1), b2 = __shfl(a0, 2);  // rows 1, 2 start (R > 1, > 2)
+        const unsigned long long rm = (1ull << R) - 1;
+        if (n0 <= 0 || f0 == 0 || !p.mcache || A1 - A0 > 64 * NEAR_PER ||
+            (__ballot(rl && n == n0 && t == t0 && f == f0) & rm) != rm)
+            continue;
+        // 2. the row cache words of rows 1.. against row 0's, and the rows' A entries
+        const int words = f0 == 1 ? span : t0;
+        const unsigned long long* s0 = p.mcache + (size_t)h * p.mc_stride;
+        bool diff = false;
+        for (int i = lane; i < (R - 1) * words; i += 64) {
+            const int r = 1 + (i >= words), q = i - (r - 1) * words;
+            const unsigned long long* s1 = p.mcache + (size_t)(h + r) * p.mc_stride;
+            diff = diff || s0[q] != s1[q] ||
+                   (f0 == 2 && reinterpret_cast<const int*>(s0 + p.mc_list)[q] != reinterpret_cast<const int*>(s1 + p.mc_list)[q]);
+        }
+        int c[NEAR_PER];
+        double v[NEAR_PER];
+        int cmin = INT_MAX, cmax = -1;
+#pragma unroll
+        for (int u = 0; u < NEAR_PER; ++u) {
+            const int j = A0 + lane + 64 * u;
+            c[u] = j < A1 ? p.Acol[j] : -1;
+            v[u] = j < A1 ? p.Aval[j] : 0.0;
+            if (c[u] >= 0) {
+                cmin = min(cmin, c[u]);
+                cmax = max(cmax, c[u]);
+            }
+        }
+        if (__ballot(diff)) continue;
+        // 3. the union row over the rows' column window (A rows need not be sorted)
+        cmin = __builtin_amdgcn_readfirstlane(wave_min(cmin));
+        cmax = __builtin_amdgcn_readfirstlane(wave_max(cmax));
+        if (cmax - cmin >= NEAR_WORDS * 64) continue;
+        const int nw = ((cmax - cmin) >> 6) + 1;
+        for (int q = lane; q < nw; q += 64) bm[q] = 0ull;
+        tm.sync();
+#pragma unroll
+        for (int u = 0; u < NEAR_PER; ++u)
+            if (c[u] >= 0) atomicOr(&bm[(c[u] - cmin) >> 6], 1ull << ((c[u] - cmin) & 63));
+        tm.sync();
+        tm.exclusive_scan(nw, [&](int q) { return (int)__popcll(bm[q]); }, [&](int q, int x) { wpre[q] = x; });
+        tm.sync();
+        const int nU = __builtin_amdgcn_readfirstlane(wpre[nw - 1] + (int)__popcll(bm[nw - 1]));
+        if (nU > NEAR_UMAX) continue;
+        for (int q = lane; q < R * nU; q += 64) uv[q] = 0.0;
+        tm.sync();
+#pragma unroll
+        for (int u = 0; u < NEAR_PER; ++u) {
+            if (c[u] < 0) continue;
+            const int j = A0 + lane + 64 * u, r = (R > 1 && j >= b1) + (R > 2 && j >= b2);
+            const int d = c[u] - cmin;
+            const int rk = wpre[d >> 6] + (int)__popcll(bm[d >> 6] & ((1ull << (d & 63)) - 1));
+            atomicAdd(&uv[r * nU + rk], v[u]);  // (duplicate columns in a row: summed, as their products)
+            p.ucol[A0 + rk] = c[u];             // (the rows that share a column write it alike)
+        }
+        tm.sync();
+        for (int q = lane; q < R * nU; q += 64) p.uval[3LL * A0 + q] = uv[q];
+        if (lane == 0) {
+            p.gna[h] = nU;
+            p.grp[h] = (unsigned char)(R | GRP_NEAR);
+        }
+        if (lane > 0 && lane < R) p.grp[h + lane] = (unsigned char)(GRP_CONT | lane);
+    }
 }
 
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
@@ -2132,7 +2313,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                int* __restrict__ list, Stats* __restrict__ stats,
                                                int dense_span_max, Published* pub, int seq, int tiny_ok,
                                                const unsigned long long* __restrict__ blkflop, int nflop, int nft,
-                                               long long* __restrict__ tslot) {
+                                               long long* __restrict__ tslot, SpecPlan sp) {
     constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
     static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
@@ -2191,15 +2372,19 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
             const int span = n ? hi - lo + 1 : 0;
             const int g = grp[i];
             // a group runs as one item when its R accumulators fit a wave bin; its
-            // members decide alike (same pattern, same sizes) and then stay out
-            const int gh = (g & GRP_CONT) ? grp[i - (g & 0x7F)] : g;
+            // members decide alike (same C pattern and sizes; flop and A length: the head's)
+            // and then stay out
+            const int hrow = (g & GRP_CONT) ? i - (g & 0x7F) : i;
+            const int gh = ((g & GRP_CONT) ? grp[hrow] : g) & GRP_RMASK;
             const int nA = Aptr[i + 1] - Aptr[i];
+            const int hflop = gh > 1 ? rflop[hrow] : rflop[i];
+            const int hnA = gh > 1 ? Aptr[hrow + 1] - Aptr[hrow] : nA;
             // tiny sort keys hold the column relative to the row's first tile in 23 bits
             const bool tok = tiny_ok && (long long)span * TILE_BITS - 1 <= TINY_NUM_NMAX;
             // numeric-first rows (k_analyze's rule) have their values: one copy list
             const int fc = nft && tok ? tiny_class(rflop[i], nA, TINY_SYM_NC) : -1;
             const int gb =
-                fc >= 0 ? -1 : num_group_bin_of(n, rflop[i], span, ctiles[i], gh, dense_span_max, nA, tok);
+                fc >= 0 ? -1 : num_group_bin_of(n, hflop, span, ctiles[i], gh, dense_span_max, hnA, tok);
             if (nft && fc < 0) tslot[i] = -1;  // (slot rows: written by the symbolic pass)
             if (gb < 0)
                 nbin = NUM_TINY + fc;
@@ -2276,6 +2461,24 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     append_block_rows<NUM_NB, PER>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
     if (pub) {
+        if (sp.out) {  // launch-ahead: do this call's bins fit the queued launches?  (SpecPlan)
+            if (threadIdx.x == 0) {
+                auto ld = [&](const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+                const long long nnzC =
+                    __hip_atomic_load(&stats->nnzC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                bool ok = ld(&stats->err) == 0 && nnzC <= sp.cap && ld(&stats->num_count[NUM_GLOBAL]) == 0;
+                for (int b = 1; b < NUM_NB; ++b) {
+                    const int c = ld(&stats->num_count[b]);
+                    sp.out[1 + b] = c;
+                    if (c > 0 && !((sp.mask >> b) & 1)) ok = false;
+                }
+                if (ld(&stats->num_count[NUM_B256]) > 0 && BLOCK_HDR + ld(&stats->num_block_need[0]) > sp.lds[0]) ok = false;
+                if (ld(&stats->num_count[NUM_B1024]) > 0 && BLOCK_HDR + ld(&stats->num_block_need[1]) > sp.lds[1]) ok = false;
+                sp.out[0] = ok;
+                __hip_atomic_store(&stats->spec_ok, (int)ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+        }
         publish_stats(stats, pub, seq);
         // the host has its copy: leave the device Stats zeroed for the next call (nothing
         // after this kernel reads them), which saves that call a memset launch
@@ -2312,8 +2515,23 @@ struct NumArgs {
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
     int* cursor;             // this launch's row cursors (block queue, guided / queued wave walks)
     SpillLists sp;           // tile lists of rows past the row cache's cap (symbolic -> numeric)
-    int qall;                // guided bins: every row from the cursor (few rows a wave)
+    int qall;                // guided bins: every row from the cursor (few rows a wave; < 0: from count)
+    int bin;                 // the launch's numeric bin
+    const int* spec;         // launch-ahead: verdict and counts (SpecPlan), else nullptr
+    const int* ucol;         // near groups' union rows (GRP_NEAR; see Work)
+    const double* uval;
+    const int* gna;
 };
+
+// Launch-ahead launches take their count from k_scan's hand-over; false: the plan did not
+// fit this call (the host launches again for the true counts), the kernel returns at once.
+__device__ __forceinline__ bool spec_take(NumArgs& a) {
+    if (!a.spec) return true;
+    if (!a.spec[0]) return false;
+    a.count = a.spec[1 + a.bin];
+    if (a.qall < 0) a.qall = a.count <= MHS_DYN16_MAX;
+    return true;
+}
 
 template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
 __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, int span, int t,
@@ -2497,9 +2715,14 @@ __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, 
         const Accum<GLOBALMEM, MODE> f{E, acc, lo, H, colbase, a.Bcol, a.Bval};
         if constexpr (GROUPED) {
             const int nAr = a1 - a0;
-            for_products_group(a0, a1, a.Acol, a.Aval, a.bmeta,
-                               nAr > 0 ? (__builtin_amdgcn_readfirstlane(a.rflop[row]) + nAr - 1) / nAr : 1, f, R,
-                               nAr, stride);
+            const int avg = nAr > 0 ? (__builtin_amdgcn_readfirstlane(a.rflop[row]) + nAr - 1) / nAr : 1;
+            // a near group walks its union row (columns at the head's A offset, R value slices
+            // nU apart from 3 * Aptr[head]): row r's value of union entry j at uv[a0 + j + r * nU]
+            // with uv = uval + 2 * a0.  (One call site: two inlined walks doubled the registers.)
+            const bool nearg = (__builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_NEAR) != 0;
+            const int nw = nearg ? __builtin_amdgcn_readfirstlane(a.gna[row]) : nAr;
+            for_products_group(a0, a0 + nw, nearg ? a.ucol : a.Acol, nearg ? a.uval + 2LL * a0 : a.Aval, a.bmeta, avg,
+                               f, R, nw, stride);
         } else {
             walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
         }
@@ -2813,7 +3036,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
         const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
         if constexpr (GROUPED)  // a group head: R rows of one pattern
             num_row<WaveTeam, false, true, MODES_ALL>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
-                                                         __builtin_amdgcn_readfirstlane((int)a.grp[row]));
+                                                         __builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_RMASK);
         else
             num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH>(tm, a, row, reg + WAVE_HDR,
                                                                              (int*)reg, nullptr);
@@ -2855,19 +3078,23 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_GRP) void k_num_wave(NumA
 #else
 __global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
 #endif
+    if (!spec_take(a)) return;
     num_wave_rows<BYTES, GROUPED, HASH>(a);
 }
 template <int BYTES>
-__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_HASH) void k_num_wave_hash(NumArgs a) {
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(BYTES > NUM_WS_BYTES ? MHS_WPE_HASH16 : MHS_WPE_HASH) void k_num_wave_hash(NumArgs a) {
+    if (!spec_take(a)) return;
     num_wave_rows<BYTES, false, true>(a);
 }
 template <int BYTES>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_DIRECT) void k_num_wave_direct(NumArgs a) {
+    if (!spec_take(a)) return;
     num_wave_rows<BYTES, false, false>(a);
 }
 
 template <int T, bool GLOBALMEM>
 __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
+    if (!spec_take(a)) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BlockTeam<T, GLOBALMEM> tm{(long long*)smem};
     char* reg = GLOBALMEM ? (a.gscratch + (long long)blockIdx.x * a.gbytes) : (smem + BLOCK_HDR);
@@ -2935,6 +3162,7 @@ struct TinyArgs {
     long long* tslot;
     long long sbase;
     int blk0[TINY_SYM_NC + 1];  // slots: class c takes blocks [blk0[c], blk0[c+1]) (sized on the host)
+    const int* spec;            // numeric launch-ahead: verdict and counts (SpecPlan), else nullptr
 };
 
 template <int W, int K, bool NUMERIC>
@@ -2945,7 +3173,7 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
     const int tb = lane & ~(W - 1);  // the team's first lane
     const unsigned long long tmask = W == 64 ? ~0ull : (((1ull << (W & 63)) - 1) << tb);
     const unsigned long long below = tmask & lanemask_lt();
-    const int count = a.count >= 0 ? a.count : a.stats->sym_count[a.bin];
+    const int count = a.spec ? a.spec[1 + a.bin] : a.count >= 0 ? a.count : a.stats->sym_count[a.bin];
     const bool slots = NUMERIC && a.sc_col != nullptr;  // numeric-first: into value slots
     const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W), bid, nb);
     extern __shared__ __attribute__((aligned(16))) char tiny_smem[];
@@ -3078,6 +3306,7 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
 
 template <int W, int K>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_TINY) void k_tiny_num(TinyArgs a) {
+    if (a.spec && !a.spec[0]) return;
     tiny_rows<W, K, true>(a, (int)blockIdx.x, (int)gridDim.x);
 }
 
@@ -3090,6 +3319,7 @@ struct TinyFused {
     int blk0[5];
 };
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(8) void k_tiny_num_small(TinyArgs a, TinyFused f) {
+    if (a.spec && !a.spec[0]) return;
     int k = 0;
     while (k + 1 < f.nclass && (int)blockIdx.x >= f.blk0[k + 1]) ++k;
     const int bid = (int)blockIdx.x - f.blk0[k], nb = f.blk0[k + 1] - f.blk0[k];
@@ -3284,12 +3514,39 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
 
 void launch_bin_list(const Csr& A, const Work& w, hipStream_t s) {
     const unsigned char* nb = w.nft ? w.nft_bin : nullptr;
+    const NearCand nc{A.ptr, A.col, w.rlo, w.rhi, (w.groups && !nb) ? w.near_list : nullptr};
     if (scan_per(A.M) == 4)
         hipLaunchKernelGGL(k_bin_list<4>, dim3((A.M + 4095) / 4096), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
-                           w.groups, w.bin_list, nb, w.stats);
+                           w.groups, w.bin_list, nb, w.stats, nc);
     else
         hipLaunchKernelGGL(k_bin_list<1>, dim3((A.M + 1023) / 1024), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
-                           w.groups, w.bin_list, nb, w.stats);
+                           w.groups, w.bin_list, nb, w.stats, nc);
+}
+
+void launch_near(const Csr& A, const Work& w, const int* Cptr, hipStream_t s) {
+    if (A.M <= 1 || !w.near_list || !w.groups || w.nft) return;
+    NearArgs p{};
+    p.Aptr = A.ptr;
+    p.Acol = A.col;
+    p.Aval = A.val;
+    p.Cptr = Cptr;
+    p.ctiles = w.ctiles;
+    p.rlo = w.rlo;
+    p.rhi = w.rhi;
+    p.rflop = w.rflop;
+    p.rtflop = w.rtflop;
+    p.mcache = w.mcache;
+    p.mc_list = w.mc_list;
+    p.mc_stride = mc_stride(w.mc_list);
+    p.list = w.near_list;
+    p.stats = w.stats;
+    p.grp = w.grp;
+    p.ucol = w.ucol;
+    p.uval = w.uval;
+    p.gna = w.gna;
+    // a persistent grid over the device-side candidate count (none: the waves return at once)
+    const int cap = (A.M / 3 + WPB - 1) / WPB;
+    hipLaunchKernelGGL(k_near, dim3(round8(cap, MHS_NEAR_GRID)), dim3(256), 0, s, p);
 }
 
 hipError_t probe_counter(unsigned long long** dev) {
@@ -3436,13 +3693,13 @@ void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, 
 }
 
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
-                          Published* pub, int seq) {
+                          Published* pub, int seq, const SpecPlan& sp) {
     // the state words were zeroed by k_analyze (SCAN_ITEMS-row blocks: enough for either width)
     const int per = scan_per(M), nb = (M + 1 + 1024 * per - 1) / (1024 * per);
 #define MHS_SCAN(P)                                                                                                \
     hipLaunchKernelGGL(k_scan<P>, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop,  \
                        w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
-                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot)
+                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, sp)
     if (per == 4) MHS_SCAN(4);
     else MHS_SCAN(1);
 #undef MHS_SCAN
@@ -3470,8 +3727,17 @@ int numeric_launches(const Stats& h) {
 // launches are dealt round-robin over them (launch i on ss[(i + 1) % nss], so the last,
 // bulk wave bins tend to stay on ss[0]): one bin's tail overlaps the next bin's bulk (the
 // reference runs its bins on 12 streams, src/Tool.cu:6-10).  Returns the mask of streams used.
+void numeric_spec_plan(const Stats& h, SpecPlan& sp) {
+    sp.mask = 0;
+    for (int b = 1; b < NUM_NB; ++b)
+        if (h.num_count[b] > 0) sp.mask |= 1 << b;
+    sp.lds[0] = block_lds(h.num_block_need[0], NUM_B256_BYTES);  // (as launch_numeric sizes them)
+    sp.lds[1] = block_lds(h.num_block_need[1], LDS_MAX - 1024);
+}
+
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
-                   double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max) {
+                   double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max,
+                   const int* spec) {
     int nl = 0, used = 0;
     auto next_stream = [&]() {
         const int k = nss > 1 ? (nl + 1) % nss : 0;
@@ -3506,6 +3772,10 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     a.grp = w.grp;
     a.cursor = w.cursors;
     a.sp = w.spill;
+    a.spec = spec;
+    a.ucol = w.ucol;
+    a.uval = w.uval;
+    a.gna = w.gna;
 
     // Numeric-first rows: their copy first (short and HBM-bound: it runs beside the long rows'
     // launches instead of behind one of them).
@@ -3544,6 +3814,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     // Largest bins first so the long rows start early.
     if (h.num_count[NUM_GLOBAL] > 0) {
         const int count = a.count = h.num_count[NUM_GLOBAL];
+        a.bin = NUM_GLOBAL;
         a.list = w.bin_list + (long long)(NUM_GLOBAL - 1) * A.M;
         a.cursor = w.cursors + NUM_GLOBAL * 8 * CURSOR_STRIDE;
         a.gbytes = align16(h.num_global_need);
@@ -3553,6 +3824,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_B1024] > 0) {
         const int count = a.count = h.num_count[NUM_B1024];
+        a.bin = NUM_B1024;
         a.list = w.bin_list + (long long)(NUM_B1024 - 1) * A.M;
         a.cursor = w.cursors + NUM_B1024 * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3561,6 +3833,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_B256] > 0) {
         const int count = a.count = h.num_count[NUM_B256];
+        a.bin = NUM_B256;
         a.list = w.bin_list + (long long)(NUM_B256 - 1) * A.M;
         a.cursor = w.cursors + NUM_B256 * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3569,9 +3842,10 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_W16H] > 0) {
         const int count = a.count = h.num_count[NUM_W16H];
+        a.bin = NUM_W16H;
         a.list = w.bin_list + (long long)(NUM_W16H - 1) * A.M;
         a.cursor = w.cursors + NUM_W16H * 8 * CURSOR_STRIDE;
-        a.qall = count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
+        a.qall = spec ? -1 : count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
         s = next_stream();
         hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_W16H_GRID)),
                            dim3(256), WPB * NUM_W16_BYTES, s, a);
@@ -3579,6 +3853,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_WSH] > 0) {
         const int count = a.count = h.num_count[NUM_WSH];
+        a.bin = NUM_WSH;
         a.list = w.bin_list + (long long)(NUM_WSH - 1) * A.M;
         a.cursor = w.cursors + NUM_WSH * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3587,6 +3862,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_W16] > 0) {
         const int count = a.count = h.num_count[NUM_W16];
+        a.bin = NUM_W16;
         a.list = w.bin_list + (long long)(NUM_W16 - 1) * A.M;
         a.cursor = w.cursors + NUM_W16 * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3606,6 +3882,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         t.Ccol = Ccol;
         t.Cval = Cval;
         t.rlo = w.rlo;
+        t.spec = spec;
         for (int c = TINY_NC - 1; c >= 4; --c) {  // 64-lane classes: kernels of their own (registers)
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;
@@ -3636,6 +3913,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_W16G] > 0) {
         const int count = a.count = h.num_count[NUM_W16G];
+        a.bin = NUM_W16G;
         a.list = w.bin_list + (long long)(NUM_W16G - 1) * A.M;
         a.cursor = w.cursors + NUM_W16G * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3644,6 +3922,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_WSG] > 0) {
         const int count = a.count = h.num_count[NUM_WSG];
+        a.bin = NUM_WSG;
         a.list = w.bin_list + (long long)(NUM_WSG - 1) * A.M;
         a.cursor = w.cursors + NUM_WSG * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3652,6 +3931,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_WS] > 0) {
         const int count = a.count = h.num_count[NUM_WS];
+        a.bin = NUM_WS;
         a.list = w.bin_list + (long long)(NUM_WS - 1) * A.M;
         a.cursor = w.cursors + NUM_WS * 8 * CURSOR_STRIDE;
         s = next_stream();

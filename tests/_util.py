@@ -246,3 +246,37 @@ def tiny_zoo(seed: int = 7, K: int = 3000, N: int = 5000):
     Acol = np.array([k for r in arows for k in r], np.int32)
     Av = rng.uniform(0.1, 1.0, len(Acol))
     return (M, K, Aptr.astype(np.int32), Acol, Av), (K, N, Bptr.astype(np.int32), Bc, Bv)
+
+
+def near_zoo(seed: int = 4):
+    """A x B for near row groups (GRP_NEAR): B a 27-point x 3-dof FEM grid, A its pattern
+    with 5 % of the off-diagonal entries dropped per row (dof triples whose A rows differ
+    by a few entries but whose C rows mostly coincide), and some rows made awkward: a far
+    column appended (unsorted, and the row's C pattern no longer matches its triple's), an
+    entry repeated (a duplicate column, summed), the row reversed (unsorted A)."""
+    from mhspgemm import synth
+    B = synth.fem_grid(12, 10, 8, seed=seed)
+    rng = np.random.default_rng(seed)
+    cols, vals, lens = [], [], []
+    for i in range(B.M):
+        c = B.col[B.ptr[i]:B.ptr[i + 1]].copy()
+        v = rng.uniform(0.1, 1.0, len(c))
+        keep = (c == i) | (rng.random(len(c)) >= 0.05)
+        c, v = c[keep], v[keep]
+        u = rng.random()
+        if u < 0.04:
+            c = np.append(c, rng.integers(0, B.M))
+            v = np.append(v, 0.5)
+        elif u < 0.07:
+            j = int(rng.integers(0, len(c)))
+            c = np.insert(c, j, c[j])
+            v = np.insert(v, j, 0.25)
+        elif u < 0.10:
+            c, v = c[::-1].copy(), v[::-1].copy()
+        cols.append(c)
+        vals.append(v)
+        lens.append(len(c))
+    ptr = np.zeros(B.M + 1, np.int64)
+    ptr[1:] = np.cumsum(lens)
+    A = (B.M, B.M, ptr.astype(np.int32), np.concatenate(cols).astype(np.int32), np.concatenate(vals))
+    return A, (B.M, B.N, B.ptr, B.col, B.val)
