@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 8
+#define MHS_ABI_VERSION 7
 
 typedef enum mhs_status {
     MHS_OK = 0,
@@ -100,13 +100,6 @@ int mhs_ctx_trim(mhs_ctx *ctx);
  *     on, rows of at most 128 products are summed during the symbolic phase into
  *     cached value slots and numeric only copies them into C (one sort instead of
  *     two; one more device-to-host hand-off per call, so big matrices only).
- *   MHS_OPT_LAUNCH_AHEAD (default 1; env MHS_LAUNCH_AHEAD=0 turns it off): a call without
- *     a timing struct on the same operands (A, B arrays and sizes) as the context's last
- *     whole-matrix call queues that call's numeric launches, and a C of its size, right
- *     behind the row_ptr scan instead of after the host has read this call's bin sizes.
- *     The scan's last block checks that this call's bins fit those launches (else they
- *     return at once and the host launches for the true sizes), so C is exact either way;
- *     C's arrays may then be larger than C.nnz entries.
  * Out of memory: when the workspace, C.ptr, the global-bin scratch or C beside them does
  * not fit, mhs_spgemm gives back every cached buffer and retries row-chunked: a counting
  * pass with the largest chunk workspace that fits sizes C; C is allocated before the
@@ -114,13 +107,10 @@ int mhs_ctx_trim(mhs_ctx *ctx);
  * returns MHS_ERR_OOM right after the counting pass when C itself does not fit, or when
  * a one-row workspace does not fit. */
 typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2, MHS_OPT_MEM_BUDGET = 3,
-                           MHS_OPT_TINY_FIRST_ROWS = 4, MHS_OPT_LAUNCH_AHEAD = 5 } mhs_option;
+                           MHS_OPT_TINY_FIRST_ROWS = 4 } mhs_option;
 int mhs_ctx_set_option(mhs_ctx *ctx, int option, int value);
 /* Calls of this context that ran row-chunked (the out-of-memory fallback). */
 long long mhs_ctx_chunked_calls(const mhs_ctx *ctx);
-/* Calls whose launch-ahead numeric ran (misses = 0) or did not fit and was launched again
- * (misses = 1). */
-long long mhs_ctx_launch_ahead_calls(const mhs_ctx *ctx, int misses);
 /* Numeric-phase durations (ms) of the last min(n, recorded) calls, oldest
  * first; waits for them.  Returns the count written, or -status on error. */
 int mhs_ctx_numeric_ms(mhs_ctx *ctx, float *out, int n);

@@ -71,17 +71,6 @@ struct mhs_ctx {
     int num_streams = 4;
     hipStream_t aux[NAUX] = {};
     hipEvent_t fork_ev = nullptr, join_ev[NAUX] = {};
-    // launch-ahead numeric (SpecPlan, MHS_OPT_LAUNCH_AHEAD): the operands and Stats of the
-    // last call that ran the whole matrix; a call on the same operands queues that call's
-    // numeric launches behind k_scan instead of waiting for its own Stats first
-    bool launch_ahead = true;
-    struct Plan {
-        bool valid = false;
-        int AM = 0, AN = 0, Annz = 0, BM = 0, BN = 0, Bnnz = 0;
-        const void* arrays[4] = {};
-        Stats h{};
-    } plan;
-    long long ahead_hits = 0, ahead_misses = 0;
 };
 
 namespace {
@@ -177,7 +166,7 @@ void pool_put(mhs_ctx* ctx, void* p) {
 
 struct Layout {
     size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, asame, grp, bin_list, scan_part, mcache,
-        stats, spec, blkflop, spill_mask, spill_key, lofs, tslot, nft_bin, near_list, ucol, uval, gna, total;
+        stats, blkflop, spill_mask, spill_key, lofs, tslot, nft_bin, near_list, nsig, ucol, uval, gna, total;
     bool near;
     long long spill_cap;
 };
@@ -192,7 +181,6 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     };
     const size_t nscan = (size_t)(M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1;
     L.stats = take(sizeof(Stats));
-    L.spec = take(SPEC_INTS * 4);
     L.btcol = take((size_t)nnzB * 4);
     L.btmask = take((size_t)nnzB * 8);
     L.bmeta = take((size_t)MB * 16);
@@ -222,6 +210,7 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     L.near = near;
     if (near) {  // near row groups: candidate list, union rows (see Work)
         L.near_list = take((size_t)M * 4);
+        L.nsig = take((size_t)M * 4);
         L.ucol = take((size_t)nnzA * 4);
         L.uval = take((size_t)nnzA * 24);
         L.gna = take((size_t)M * 4);
@@ -296,12 +285,12 @@ Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, int Bn, int
     w.tslot = (long long*)(ctx->ws + L.tslot);
     if (L.near) {
         w.near_list = (int*)(ctx->ws + L.near_list);
+        w.nsig = (unsigned*)(ctx->ws + L.nsig);
         w.ucol = (int*)(ctx->ws + L.ucol);
         w.uval = (double*)(ctx->ws + L.uval);
         w.gna = (int*)(ctx->ws + L.gna);
     }
     w.stats = (Stats*)(ctx->ws + L.stats);
-    w.spec = (int*)(ctx->ws + L.spec);
     w.gscratch = ctx->gscratch;
     w.gscratch_bytes = ctx->gscratch_bytes;
     return w;
@@ -325,7 +314,7 @@ int front_pass(mhs_ctx* ctx, const Csr& a, const Csr& b, Work& w, int* Cptr, boo
     if (mask) launch_mask_b(b, w, s);
     launch_analyze(a, w, b.M, s, Cptr);
     launch_symbolic_common(a, b, w, a.M, b.N, Cptr, s);
-    launch_symbolic_rare(a, w, a.M, b.N, Cptr, s);
+    launch_symbolic_rare(a, w, a.M, b.N, Cptr, s, false);
     const int seq = ++ctx->seq;
     launch_scan_classify(a.M, w, Cptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
     MHS_HIP(hipGetLastError());
@@ -343,9 +332,8 @@ int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h);
 constexpr int NUM_GLOBAL_GRID = 128;
 
 // The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
-// the aux streams, which join the call's stream again; spec: launch-ahead (SpecPlan).
-int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out,
-                const int* spec) {
+// the aux streams, which join the call's stream again.
+int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out) {
     hipStream_t s = ctx->stream;
     // several heavy bins: deal them over the aux streams (fork/join costs ~10-20 us,
     // so only when there are at least 3 launches of a product worth it)
@@ -360,7 +348,7 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
         }
     }
     const int used =
-        launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID, ctx->dense_span_max, spec);
+        launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID, ctx->dense_span_max);
     MHS_HIP(hipGetLastError());
     for (int i = 1; i < nss; ++i)
         if (used & (1 << i)) {
@@ -368,23 +356,6 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
             MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[i - 1], 0));
         }
     return MHS_OK;
-}
-
-// Launch-ahead applies: same operands as the plan's call, whose numeric pass had no global
-// bin (its scratch is sized from the Stats) and a non-empty C.
-bool plan_matches(const mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B) {
-    const auto& p = ctx->plan;
-    return p.valid && p.AM == A->M && p.AN == A->N && p.Annz == A->nnz && p.BM == B->M && p.BN == B->N &&
-           p.Bnnz == B->nnz && p.arrays[0] == A->ptr && p.arrays[1] == A->col && p.arrays[2] == B->ptr &&
-           p.arrays[3] == B->col && p.h.nnzC > 0 && p.h.num_count[NUM_GLOBAL] == 0;
-}
-
-void keep_plan(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, const Stats& h) {
-    auto& p = ctx->plan;
-    p.valid = true;
-    p.AM = A->M, p.AN = A->N, p.Annz = A->nnz, p.BM = B->M, p.BN = B->N, p.Bnnz = B->nnz;
-    p.arrays[0] = A->ptr, p.arrays[1] = A->col, p.arrays[2] = B->ptr, p.arrays[3] = B->col;
-    p.h = h;
 }
 
 int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h) {
@@ -590,7 +561,6 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (getenv("MHS_NFT_NO_SLOTS")) ctx->nft_slots = false;
     if (const char* e = getenv("MHS_SYM_FORK")) ctx->sym_fork = atoi(e) != 0;
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
-    if (const char* e = getenv("MHS_LAUNCH_AHEAD")) ctx->launch_ahead = atoi(e) != 0;
     *out = ctx;
     return MHS_OK;
 }
@@ -764,65 +734,33 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     if (((w.nft && other > 0) || ctx->sym_fork) && ctx->num_streams > 1 && ctx->aux[0]) {
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
-        launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0]);
+        launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0], false);
         launch_symbolic_common(a, b, w, M, N, out.ptr, s);
         MHS_HIP(hipEventRecord(ctx->join_ev[0], ctx->aux[0]));
         MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[0], 0));
+        launch_near(a, w, out.ptr, s);
     } else {
         launch_symbolic_common(a, b, w, M, N, out.ptr, s);
-        launch_symbolic_rare(a, w, M, N, out.ptr, s);
+        launch_symbolic_rare(a, w, M, N, out.ptr, s, true);  // (+ near row groups)
     }
-    launch_near(a, w, out.ptr, s);
     MHS_HIP(hipGetLastError());
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
     Stats h;
-    const int nring = (int)ctx->nev.size() / 2;
-    const int slot = nring ? (int)(ctx->ncalls % nring) : 0;
-    bool ahead = false;  // launch-ahead numeric queued (SpecPlan)
     if (M > 0) {
-        // launch-ahead: the same operands as the last call's -- queue its numeric launches
-        // (C of its size) behind k_scan, which checks that they fit this call's bins
-        SpecPlan sp{};
-        if (ctx->launch_ahead && !timed && !probe && plan_matches(ctx, A, B)) {
-            if (alloc_c(ctx, &out, ctx->plan.h.nnzC) == hipSuccess) {
-                ahead = true;
-                numeric_spec_plan(ctx->plan.h, sp);
-                sp.out = w.spec;
-                sp.cap = ctx->plan.h.nnzC;
-            } else {
-                (void)hipGetLastError();
-                out.col = nullptr;
-                out.val = nullptr;
-            }
-        }
         // the numeric bin offsets kernel publishes Stats to pinned host memory; the
         // host spins on the sequence number (no stream sync, no interrupt wake-up)
         const int seq = ++ctx->seq;
-        launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq, sp);
+        launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
         MHS_HIP(hipGetLastError());
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
-        if (ahead) {
-            if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
-            rc = run_numeric(ctx, a, b, w, ctx->plan.h, out, w.spec);
-        }
-        if (!rc) rc = wait_published(ctx, s, ctx->pub, seq);
+        rc = wait_published(ctx, s, ctx->pub, seq);
         if (rc) {
-            mhs_ctx_recycle(ctx, &out);
+            pool_put(ctx, out.ptr);
             return rc;
         }
         memcpy(&h, (const void*)&ctx->pub->stats, sizeof(Stats));
         ctx->stats_zero = true;  // k_scan's last block cleared them after publishing
-        if (ahead && !h.spec_ok) {  // the plan did not fit: those launches returned at once
-            pool_put(ctx, out.col);
-            pool_put(ctx, out.val);
-            out.col = nullptr;
-            out.val = nullptr;
-            ahead = false;
-            ++ctx->ahead_misses;
-        } else if (ahead) {
-            ++ctx->ahead_hits;
-        }
     } else {
         MHS_HIP(hipGetLastError());
         MHS_HIP(hipMemcpyAsync(ctx->h_stats, w.stats, sizeof(Stats), hipMemcpyDeviceToHost, s));
@@ -841,11 +779,9 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     }
     out.nnz = (int)h.nnzC;
 
-    if (M > 0 && !probe) keep_plan(ctx, A, B, h);
-
     // ---- Malloc_C_col_val ---------------------------------------------------------------
     const auto T5 = std::chrono::steady_clock::now();
-    if (!ahead) {
+    {
         const hipError_t e = alloc_c(ctx, &out, out.nnz);
         if (e != hipSuccess) {
             pool_put(ctx, out.ptr);
@@ -855,7 +791,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
             return fail_hip(ctx, e, "allocating C.col/C.val");
         }
     }
-    rc = ahead ? MHS_OK : ensure_gscratch(ctx, w, h);
+    rc = ensure_gscratch(ctx, w, h);
     if (rc) {
         mhs_ctx_recycle(ctx, &out);
         (void)hipGetLastError();
@@ -866,14 +802,14 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
 
     // ---- Numeric -------------------------------------------------------------------------
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
-    if (!ahead) {
-        if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
-        if (out.nnz > 0) {
-            rc = run_numeric(ctx, a, b, w, h, out, nullptr);
-            if (rc) {
-                mhs_ctx_recycle(ctx, &out);
-                return rc;
-            }
+    const int nring = (int)ctx->nev.size() / 2;
+    const int slot = nring ? (int)(ctx->ncalls % nring) : 0;
+    if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
+    if (out.nnz > 0) {
+        rc = run_numeric(ctx, a, b, w, h, out);
+        if (rc) {
+            mhs_ctx_recycle(ctx, &out);
+            return rc;
         }
     }
     MHS_HIP(hipGetLastError());
@@ -966,19 +902,12 @@ int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
     case MHS_OPT_TINY_FIRST_ROWS:
         ctx->nft_min_m = value;
         return MHS_OK;
-    case MHS_OPT_LAUNCH_AHEAD:
-        ctx->launch_ahead = value != 0;
-        return MHS_OK;
     default:
         return fail(ctx, MHS_ERR_INVALID, "unknown option");
     }
 }
 
 long long mhs_ctx_chunked_calls(const mhs_ctx* ctx) { return ctx ? ctx->chunked_calls : -1; }
-
-long long mhs_ctx_launch_ahead_calls(const mhs_ctx* ctx, int misses) {
-    return ctx ? (misses ? ctx->ahead_misses : ctx->ahead_hits) : -1;
-}
 
 int mhs_ctx_numeric_ms(mhs_ctx* ctx, float* out, int n) {
     if (!ctx || (!out && n > 0)) return -MHS_ERR_INVALID;

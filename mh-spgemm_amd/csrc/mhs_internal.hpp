@@ -102,13 +102,12 @@ constexpr int RG_MAX = 3;
 constexpr int RG_BREAK = 96;  // a multiple of 2, 3, 4 and 6: dof blocks of those sizes stay whole
 constexpr int GRP_CONT = 0x80;
 // Near row groups: consecutive rows whose A patterns differ by a few entries (k_bin_list's
-// candidates: same C tile span, A lengths within NEAR_DLEN, same first or last column) and
+// candidates: rows of the small-table wave bin with the same C tile span and first column) and
 // whose C patterns turn out equal (k_near, after the symbolic pass counted each row on its
 // own).  Their numeric runs as a row group over the union of their A rows (ucol / uval:
 // columns once, R values each, 0 where a row lacks the column).  Head: R | GRP_NEAR.
 constexpr int GRP_NEAR = 0x40;
 constexpr int GRP_RMASK = 0x3F;
-constexpr int NEAR_DLEN = 16;
 constexpr int NEAR_WORDS = 256;   // union rows: A columns within a window of NEAR_WORDS * 64
 constexpr int NEAR_UMAX = 128;    // ... and at most this many union entries
 
@@ -156,7 +155,6 @@ struct Stats {
     unsigned long long an_slots;   // numeric-first probe: the candidates' slot entries,
     unsigned long long an_other;   // rows with products past the tiny classes,
     int an_done;                   // and k_probe_publish blocks finished
-    int spec_ok;                   // the launch-ahead numeric ran this call's bins (SpecPlan)
     int near_heads;                // near-group candidates listed by k_bin_list (k_near's work)
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
@@ -166,20 +164,6 @@ struct Published {
     int seq;
     int pad[3];
 };
-// Launch-ahead numeric (mhs_api.cpp): a call whose operands match the previous call's
-// queues that call's numeric launches right behind k_scan, before the host has this call's
-// Stats.  k_scan's last block checks that this call's bins fit those launches -- C capacity,
-// launched bins, the block kernels' LDS, no global bin, no input error -- and hands the
-// counts over: out[0] = fits, out[1 + b] = bin b's count.  The numeric kernels take their
-// counts from `out` and return at once when it does not fit (the host then launches for
-// the true counts).  Grids are persistent walks, so any count runs on any grid.
-struct SpecPlan {
-    int* out;       // nullptr: no launch-ahead this call
-    long long cap;  // C entries allocated
-    int mask;       // bins launched (bit b)
-    int lds[2];     // dynamic LDS of the NUM_B256 / NUM_B1024 launches
-};
-constexpr int SPEC_INTS = 1 + NBINS;
 constexpr int SAME_PATTERN = 0x40000000;  // bmeta.z flag: B row repeats row-1's columns
 constexpr int ERR_UNSORTED = 1;
 constexpr int ERR_COL_RANGE = 2;
@@ -359,6 +343,7 @@ struct Work {
     // at the head's A offset (ucol: nnz(A) ints; uval: 3 nnz(A) doubles, values of row r at
     // 3 * Aptr[head] + r * nU), union length per head
     int* near_list;
+    unsigned* nsig;  // M: k_analyze's near-link signature of every row
     int* ucol;
     double* uval;
     int* gna;
@@ -381,7 +366,6 @@ struct Work {
     int mc_list;                  // list cap (see mlisted)
     SpillArea spill;              // tile lists of rows past mc_list (symbolic -> numeric)
     Stats* stats;
-    int* spec;         // SPEC_INTS: launch-ahead verdict and counts (k_scan -> numeric)
     void* gscratch;    // global-bin scratch
     size_t gscratch_bytes;
 };
@@ -396,17 +380,15 @@ void launch_bin_list(const Csr& A, const Work& w, hipStream_t s);
 int analyze_blocks(long long nnzA, int M);
 
 void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s);
-void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s);
+// with_near: its phase 0 checks the near row-group candidates (after k_sym_common on the
+// same stream); else launch_near does, once both symbolic launches are done
+void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, bool with_near);
 // near row groups: verify k_bin_list's candidates after the symbolic pass, build union rows
 void launch_near(const Csr& A, const Work& w, const int* Cptr, hipStream_t s);
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
-                          Published* pub, int seq, const SpecPlan& sp = SpecPlan{});
-// spec != nullptr: launch-ahead (counts from spec; see SpecPlan), grids and LDS from h
+                          Published* pub, int seq);
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
-                   int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max,
-                   const int* spec = nullptr);
-// the bins and block-kernel LDS launch_numeric launches for h (launch-ahead: k_scan checks against them)
-void numeric_spec_plan(const Stats& h, SpecPlan& sp);
+                   int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max);
 // numeric launches a call makes for these bin counts (the 32-lane tiny classes share one)
 int numeric_launches(const Stats& h);
 size_t sym_global_bytes_per_block(int N);

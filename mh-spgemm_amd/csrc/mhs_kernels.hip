@@ -850,10 +850,12 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
                                                  int* __restrict__ rhi, int* __restrict__ ctiles,
                                                  unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
                                                  unsigned char* __restrict__ asame, int& err,
-                                                 unsigned char* __restrict__ nft_bin, int& nslots, int& nother) {
+                                                 unsigned char* __restrict__ nft_bin, int& nslots, int& nother,
+                                                 unsigned* __restrict__ nsig) {
     const int gl = lane_id() & (G - 1);
     long long flop = 0, tflop = 0;
     int lo = INT_MAX, hi = -1;
+    int kfirst = -1;  // the row's first A column (lane 0 of the group)
     bool differ = true;  // row's column pattern differs from row-1's (row groups)
     bool bad = false;    // an A column outside [0, B.M): the row is never walked (MHS_ERR_INVALID)
     if (valid) {
@@ -866,6 +868,7 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
             const int k = Acol[j];
             const int kp = Acol[j - dp];  // unconditional: stays in [0, nnz(A)); a guarded load would serialise
             differ = differ || kp != k;
+            if (j == s) kfirst = k;
             if (k < 0 || k >= MB) {
                 err = ERR_ACOL_RANGE;
                 bad = true;
@@ -903,6 +906,14 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         const int tc = tiny_class_sym(f, nA);
         const int bin = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
+        // near row-group signature (k_bin_list links rows whose signatures match: the same
+        // C tile span and first A column, both in the small-table wave bin); a collision only
+        // adds a candidate that k_sym_rare's check turns down
+        if (nsig)
+            nsig[row] = (bin == SYM_WAVE && nA >= 8 && !bad)
+                            ? (((unsigned)lo * 0x9E3779B1u) ^ ((unsigned)hi * 0x85EBCA77u) ^
+                               ((unsigned)kfirst * 0xC2B2AE3Du)) | 1u
+                            : 0u;
         if (nft_bin) {
             // numeric-first candidates: the numeric classes 0..3, whose sort keys hold the
             // column relative to the row's first tile (23 bits); a wider row counts in a table
@@ -939,7 +950,7 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
                                                  unsigned char* __restrict__ asame,
                                                  Stats* __restrict__ stats,
                                                  unsigned long long* __restrict__ lb_state, int nlb,
-                                                 unsigned char* __restrict__ nft_bin) {
+                                                 unsigned char* __restrict__ nft_bin, unsigned* __restrict__ nsig) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
@@ -950,13 +961,13 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
     bool lng = false;
     if constexpr (G < 64) lng = valid && Aptr[row + 1] - Aptr[row] > AN_LONG * G;
     long long flop = analyze_row<G>(row, valid && !lng, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
-                                    ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother);
+                                    ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig);
     flop = gl == 0 ? flop : 0;
     if constexpr (G < 64) {
         for (unsigned long long lb = __ballot(lng && gl == 0); lb; lb &= lb - 1) {
             const int r = __shfl(row, __builtin_ctzll(lb));
             const long long f = analyze_row<64>(r, true, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
-                                                ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother);
+                                                ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig);
             flop += lane == 0 ? f : 0;
         }
     }
@@ -1947,12 +1958,154 @@ __device__ bool sym_row_bitmap(const BlockTeam<1024, false>& tm, const SymArgs& 
     return true;
 }
 
-__global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a) {
+// Near groups (k_bin_list's candidate list), one wave per candidate after the symbolic
+// pass: the rows' C patterns must be equal -- counts, tile spans, and the row cache's tile
+// masks (direct-mapped tables only: their lists come out in tile order) -- else the rows
+// stay alone.  A verified group gets its union row: the rows' A columns marked in a bitmap
+// over their column window, ranked by prefix popcounts; R value slices (0 where a row lacks
+// the column) staged in LDS and copied out.  Then grp marks it (head R | GRP_NEAR).
+struct NearArgs {
+    const int* Aptr;
+    const int* Acol;
+    const double* Aval;
+    const int* Cptr;  // the symbolic counts (before the scan)
+    const int* ctiles;
+    const int* rlo;
+    const int* rhi;
+    const int* rflop;
+    const int* rtflop;
+    const unsigned long long* mcache;
+    int mc_list, mc_stride;
+    const int* list;
+    const Stats* stats;
+    unsigned char* grp;
+    int* ucol;
+    double* uval;
+    int* gna;
+};
+#ifndef MHS_NEAR_GRID
+#define MHS_NEAR_GRID 2048  // k_near's block cap
+#endif
+constexpr int NEAR_PER = 4;  // A entries a lane holds: a group's R rows of at most 256 entries
+constexpr int NEAR_LDS = NEAR_WORDS * 12 + RG_MAX * NEAR_UMAX * 8;  // a wave's bitmap, word prefixes, values
+static_assert(16 * NEAR_LDS <= LDS_MAX_C - 1024, "k_sym_rare's 16 waves hold their near-group regions");
+// The candidate groups gw, gw + nw, ... of the list (one wave each).
+__device__ void near_groups(const NearArgs& p, char* lds, int gw, int nwaves) {
+    unsigned long long* bm = (unsigned long long*)lds;
+    int* wpre = (int*)(bm + NEAR_WORDS);
+    double* uv = (double*)(wpre + NEAR_WORDS);
+    const int lane = lane_id();
+    const WaveTeam tm;
+    const int count = __hip_atomic_load(&p.stats->near_heads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every step's loads are independent of each other: three round trips per group
+    for (int li = gw; li < count; li += nwaves) {
+        const int e = __builtin_amdgcn_readfirstlane(p.list[li]);
+        const int h = e >> 2, R = e & 3;
+        // 1. the rows' scalars, lane r for row h + r
+        const bool rl = lane < R;
+        int n = 0, t = 0, tf = 0, fl = 0, a0 = 0, a1 = 0;
+        if (rl) {
+            n = p.Cptr[h + lane];
+            t = p.ctiles[h + lane];
+            tf = p.rtflop[h + lane];
+            fl = p.rflop[h + lane];
+            a0 = p.Aptr[h + lane];
+            a1 = p.Aptr[h + lane + 1];
+        }
+        const int lo = __builtin_amdgcn_readfirstlane(p.rlo[h]);
+        const int span = __builtin_amdgcn_readfirstlane(p.rhi[h]) - lo + 1;
+        // the row cache form of each row's C pattern (1: masks over the span, 2: a tile list)
+        const int f = !rl || !sym_direct(span, tf) || tiny_class_sym(fl, a1 - a0) >= 0 ? 0
+                      : mcached(span, tf)                                              ? 1
+                      : mlisted(span, tf, t, p.mc_list)                                ? 2
+                                                                                       : 0;
+        const int n0 = __builtin_amdgcn_readfirstlane(n), t0 = __builtin_amdgcn_readfirstlane(t);
+        const int f0 = __builtin_amdgcn_readfirstlane(f);
+        const int A0 = __builtin_amdgcn_readfirstlane(a0), A1 = __shfl(a1, R - 1);
+        const int b1 = __shfl(a0, 1), b2 = __shfl(a0, 2);  // rows 1, 2 start (R > 1, > 2)
+        const unsigned long long rm = (1ull << R) - 1;
+        if (n0 <= 0 || f0 == 0 || !p.mcache || A1 - A0 > 64 * NEAR_PER ||
+            (__ballot(rl && n == n0 && t == t0 && f == f0) & rm) != rm)
+            continue;
+        // 2. the row cache words of rows 1.. against row 0's, and the rows' A entries
+        const int words = f0 == 1 ? span : t0;
+        const unsigned long long* s0 = p.mcache + (size_t)h * p.mc_stride;
+        bool diff = false;
+        for (int i = lane; i < (R - 1) * words; i += 64) {
+            const int r = 1 + (i >= words), q = i - (r - 1) * words;
+            const unsigned long long* s1 = p.mcache + (size_t)(h + r) * p.mc_stride;
+            diff = diff || s0[q] != s1[q] ||
+                   (f0 == 2 && reinterpret_cast<const int*>(s0 + p.mc_list)[q] != reinterpret_cast<const int*>(s1 + p.mc_list)[q]);
+        }
+        int c[NEAR_PER];
+        double v[NEAR_PER];
+        int cmin = INT_MAX, cmax = -1;
+#pragma unroll
+        for (int u = 0; u < NEAR_PER; ++u) {
+            const int j = A0 + lane + 64 * u;
+            c[u] = j < A1 ? p.Acol[j] : -1;
+            v[u] = j < A1 ? p.Aval[j] : 0.0;
+            if (c[u] >= 0) {
+                cmin = min(cmin, c[u]);
+                cmax = max(cmax, c[u]);
+            }
+        }
+        if (__ballot(diff)) continue;
+        // 3. the union row over the rows' column window (A rows need not be sorted)
+        cmin = __builtin_amdgcn_readfirstlane(wave_min(cmin));
+        cmax = __builtin_amdgcn_readfirstlane(wave_max(cmax));
+        if (cmax - cmin >= NEAR_WORDS * 64) continue;
+        const int nw = ((cmax - cmin) >> 6) + 1;
+        for (int q = lane; q < nw; q += 64) bm[q] = 0ull;
+        tm.sync();
+#pragma unroll
+        for (int u = 0; u < NEAR_PER; ++u)
+            if (c[u] >= 0) atomicOr(&bm[(c[u] - cmin) >> 6], 1ull << ((c[u] - cmin) & 63));
+        tm.sync();
+        tm.exclusive_scan(nw, [&](int q) { return (int)__popcll(bm[q]); }, [&](int q, int x) { wpre[q] = x; });
+        tm.sync();
+        const int nU = __builtin_amdgcn_readfirstlane(wpre[nw - 1] + (int)__popcll(bm[nw - 1]));
+        if (nU > NEAR_UMAX) continue;
+        for (int q = lane; q < R * nU; q += 64) uv[q] = 0.0;
+        tm.sync();
+#pragma unroll
+        for (int u = 0; u < NEAR_PER; ++u) {
+            if (c[u] < 0) continue;
+            const int j = A0 + lane + 64 * u, r = (R > 1 && j >= b1) + (R > 2 && j >= b2);
+            const int d = c[u] - cmin;
+            const int rk = wpre[d >> 6] + (int)__popcll(bm[d >> 6] & ((1ull << (d & 63)) - 1));
+            atomicAdd(&uv[r * nU + rk], v[u]);  // (duplicate columns in a row: summed, as their products)
+            p.ucol[A0 + rk] = c[u];             // (the rows that share a column write it alike)
+        }
+        tm.sync();
+        for (int q = lane; q < R * nU; q += 64) p.uval[3LL * A0 + q] = uv[q];
+        if (lane == 0) {
+            p.gna[h] = nU;
+            p.grp[h] = (unsigned char)(R | GRP_NEAR);
+        }
+        if (lane > 0 && lane < R) p.grp[h + lane] = (unsigned char)(GRP_CONT | lane);
+    }
+}
+
+// (the symbolic rare bins on an aux stream: the candidates checked by a launch of their own)
+__global__ __launch_bounds__(256) void k_near(NearArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[WPB * NEAR_LDS];
+    const int w = threadIdx.x >> 6;
+    near_groups(p, lds + w * NEAR_LDS, (int)blockIdx.x * WPB + w, (int)gridDim.x * WPB);
+}
+
+__global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a, NearArgs np) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int4* stage = (int4*)(smem + 1024);
     BlockTeam<1024, false> tm{(long long*)smem};
     TileEntry* E = (TileEntry*)(smem + BLOCK_HDR);
     __shared__ int qslot;
+    // phase 0: near row groups (their rows are k_sym_common's, done before this launch)
+    if (np.list) {
+        near_groups(np, smem + (threadIdx.x >> 6) * NEAR_LDS, (int)blockIdx.x * 16 + (int)(threadIdx.x >> 6),
+                    (int)gridDim.x * 16);
+        __syncthreads();
+    }
 #pragma unroll 1
     for (int bin = SYM_GLOBAL; bin >= SYM_B1024; --bin) {
         const int count = a.stats->sym_count[bin];
@@ -2057,11 +2210,8 @@ __global__ __launch_bounds__(1024) void k_probe_publish(const unsigned long long
 
 // Near-group candidates (k_bin_list): the A rows the link test reads
 struct NearCand {
-    const int* Aptr;
-    const int* Acol;
-    const int* rlo;
-    const int* rhi;
-    int* list;  // nullptr: no near groups
+    const unsigned* nsig;  // k_analyze's signatures
+    int* list;             // nullptr: no near groups
 };
 
 template <int PER>
@@ -2071,20 +2221,32 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
                                                    int* __restrict__ list, const unsigned char* __restrict__ nft_bin,
                                                    Stats* __restrict__ stats, NearCand nc) {
     __shared__ unsigned char binof[1024 * PER];
-    const int lane = lane_id();
-    // link of row r to row r-1: 1 = the same A pattern, 2 = a near candidate (see GRP_NEAR), 0 = none
-    auto link = [&](long long r) -> int {
-        if (asame[r]) return 1;
-        if (!nc.list || r == 0) return 0;
-        const int b0 = bin_id[r], b1 = bin_id[r - 1];
-        const bool t0 = b0 == SYM_NONE || (b0 >= SYM_TINY && b0 < SYM_TINY + TINY_NC);
-        const bool t1 = b1 == SYM_NONE || (b1 >= SYM_TINY && b1 < SYM_TINY + TINY_NC);
-        if (t0 || t1 || nc.rlo[r] != nc.rlo[r - 1] || nc.rhi[r] != nc.rhi[r - 1]) return 0;
-        const int s0 = nc.Aptr[r - 1], s1 = nc.Aptr[r], s2 = nc.Aptr[r + 1];
-        const int l0 = s1 - s0, l1 = s2 - s1;
-        if (l0 < 8 || l1 < 8 || l1 - l0 > NEAR_DLEN || l0 - l1 > NEAR_DLEN) return 0;
-        return (nc.Acol[s0] == nc.Acol[s1] || nc.Acol[s1 - 1] == nc.Acol[s2 - 1]) ? 2 : 0;
-    };
+    // links of rows [blk0 - RG_BREAK, blk0 + ITEMS + RG_MAX): a row's group reads its run back
+    // to the last RG_BREAK boundary and its group forward
+    constexpr int LK = 1024 * PER + RG_BREAK + RG_MAX;
+    __shared__ unsigned char lk_s[LK];
+    __shared__ int ncand_s, nbase_s;  // the block's near candidates: one counter add per block
+    if (threadIdx.x == 0) ncand_s = 0;
+    const long long lbase = (long long)blockIdx.x * (1024 * PER) - RG_BREAK;
+    // link of row r to row r-1: 1 = the same A pattern, 2 = a near candidate (see GRP_NEAR;
+    // rows of the small-table wave bin only: k_sym_rare checks them after k_sym_common), 0 = none
+    for (int j = threadIdx.x; j < LK; j += 1024) {
+        const long long r = lbase + j;
+        int l = 0;
+        if (r >= 0 && r < M) {
+            if (asame[r]) {
+                l = 1;
+            } else if (nc.list && r > 0 && !asame[r - 1] && (r + 1 >= M || !asame[r + 1])) {
+                // (rows of same-pattern runs stay out: a near link would shift their groups)
+                const unsigned g1 = nc.nsig[r];
+                l = g1 != 0u && g1 == nc.nsig[r - 1] ? 2 : 0;
+            }
+        }
+        lk_s[j] = (unsigned char)l;
+    }
+    __syncthreads();
+    auto link = [&](long long r) -> int { return lk_s[r - lbase]; };
+    int cand_e[PER], cand_n = 0;
     for (int j = threadIdx.x; j < 1024 * PER; j += 1024) {
         const long long i = (long long)blockIdx.x * (1024 * PER) + j;
         unsigned char b = 0;
@@ -2120,146 +2282,15 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
             grp[i] = (unsigned char)g;
             b = (g & GRP_CONT) ? 0 : bi;
         }
-        const unsigned long long bal = __ballot(cand);
-        if (bal) {  // one counter add per wave
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&stats->near_heads, __popcll(bal));
-            base = __shfl(base, 0);
-            if (cand) nc.list[base + __popcll(bal & lanemask_lt())] = (int)(i * 4 + cR);
-        }
+        if (cand) cand_e[cand_n++] = (int)(i * 4 + cR);
         binof[j] = b;
     }
+    int at = cand_n ? atomicAdd(&ncand_s, cand_n) : 0;
     __syncthreads();
+    if (threadIdx.x == 0 && ncand_s) nbase_s = atomicAdd(&stats->near_heads, ncand_s);
+    __syncthreads();
+    for (int q = 0; q < cand_n; ++q) nc.list[nbase_s + at + q] = cand_e[q];
     append_block_rows<SYM_NB, PER>(binof, M, stats->sym_count, list, (int)blockIdx.x);
-}
-
-// Near groups (k_bin_list's candidate list), one wave per candidate after the symbolic
-// pass: the rows' C patterns must be equal -- counts, tile spans, and the row cache's tile
-// masks (direct-mapped tables only: their lists come out in tile order) -- else the rows
-// stay alone.  A verified group gets its union row: the rows' A columns marked in a bitmap
-// over their column window, ranked by prefix popcounts; R value slices (0 where a row lacks
-// the column) staged in LDS and copied out.  Then grp marks it (head R | GRP_NEAR).
-struct NearArgs {
-    const int* Aptr;
-    const int* Acol;
-    const double* Aval;
-    const int* Cptr;  // the symbolic counts (before the scan)
-    const int* ctiles;
-    const int* rlo;
-    const int* rhi;
-    const int* rflop;
-    const int* rtflop;
-    const unsigned long long* mcache;
-    int mc_list, mc_stride;
-    const int* list;
-    const Stats* stats;
-    unsigned char* grp;
-    int* ucol;
-    double* uval;
-    int* gna;
-};
-#ifndef MHS_NEAR_GRID
-#define MHS_NEAR_GRID 2048  // k_near's block cap
-#endif
-constexpr int NEAR_PER = 4;  // A entries a lane holds: a group's R rows of at most 256 entries
-__global__ __launch_bounds__(256) void k_near(NearArgs p) {
-    __shared__ unsigned long long bm_s[WPB][NEAR_WORDS];
-    __shared__ int wpre_s[WPB][NEAR_WORDS];
-    __shared__ double uv_s[WPB][RG_MAX * NEAR_UMAX];
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    unsigned long long* bm = bm_s[w];
-    int* wpre = wpre_s[w];
-    double* uv = uv_s[w];
-    const WaveTeam tm;
-    const int count = __hip_atomic_load(&p.stats->near_heads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // every step's loads are independent of each other: three round trips per group
-    for (int li = (int)blockIdx.x * WPB + w; li < count; li += (int)gridDim.x * WPB) {
-        const int e = __builtin_amdgcn_readfirstlane(p.list[li]);
-        const int h = e >> 2, R = e & 3;
-        // 1. the rows' scalars, lane r for row h + r
-        const bool rl = lane < R;
-        int n = 0, t = 0, tf = 0, fl = 0, a0 = 0, a1 = 0;
-        if (rl) {
-            n = p.Cptr[h + lane];
-            t = p.ctiles[h + lane];
-            tf = p.rtflop[h + lane];
-            fl = p.rflop[h + lane];
-            a0 = p.Aptr[h + lane];
-            a1 = p.Aptr[h + lane + 1];
-        }
-        const int lo = __builtin_amdgcn_readfirstlane(p.rlo[h]);
-        const int span = __builtin_amdgcn_readfirstlane(p.rhi[h]) - lo + 1;
-        // the row cache form of each row's C pattern (1: masks over the span, 2: a tile list)
-        const int f = !rl || !sym_direct(span, tf) || tiny_class_sym(fl, a1 - a0) >= 0 ? 0
-                      : mcached(span, tf)                                              ? 1
-                      : mlisted(span, tf, t, p.mc_list)                                ? 2
-                                                                                       : 0;
-        const int n0 = __builtin_amdgcn_readfirstlane(n), t0 = __builtin_amdgcn_readfirstlane(t);
-        const int f0 = __builtin_amdgcn_readfirstlane(f);
-        const int A0 = __builtin_amdgcn_readfirstlane(a0), A1 = __shfl(a1, R - 1);
-        const int b1 = __shfl(a0, 1), b2 = __shfl(a0, 2);  // rows 1, 2 start (R > 1, > 2)
-        const unsigned long long rm = (1ull << R) - 1;
-        if (n0 <= 0 || f0 == 0 || !p.mcache || A1 - A0 > 64 * NEAR_PER ||
-            (__ballot(rl && n == n0 && t == t0 && f == f0) & rm) != rm)
-            continue;
-        // 2. the row cache words of rows 1.. against row 0's, and the rows' A entries
-        const int words = f0 == 1 ? span : t0;
-        const unsigned long long* s0 = p.mcache + (size_t)h * p.mc_stride;
-        bool diff = false;
-        for (int i = lane; i < (R - 1) * words; i += 64) {
-            const int r = 1 + (i >= words), q = i - (r - 1) * words;
-            const unsigned long long* s1 = p.mcache + (size_t)(h + r) * p.mc_stride;
-            diff = diff || s0[q] != s1[q] ||
-                   (f0 == 2 && reinterpret_cast<const int*>(s0 + p.mc_list)[q] != reinterpret_cast<const int*>(s1 + p.mc_list)[q]);
-        }
-        int c[NEAR_PER];
-        double v[NEAR_PER];
-        int cmin = INT_MAX, cmax = -1;
-#pragma unroll
-        for (int u = 0; u < NEAR_PER; ++u) {
-            const int j = A0 + lane + 64 * u;
-            c[u] = j < A1 ? p.Acol[j] : -1;
-            v[u] = j < A1 ? p.Aval[j] : 0.0;
-            if (c[u] >= 0) {
-                cmin = min(cmin, c[u]);
-                cmax = max(cmax, c[u]);
-            }
-        }
-        if (__ballot(diff)) continue;
-        // 3. the union row over the rows' column window (A rows need not be sorted)
-        cmin = __builtin_amdgcn_readfirstlane(wave_min(cmin));
-        cmax = __builtin_amdgcn_readfirstlane(wave_max(cmax));
-        if (cmax - cmin >= NEAR_WORDS * 64) continue;
-        const int nw = ((cmax - cmin) >> 6) + 1;
-        for (int q = lane; q < nw; q += 64) bm[q] = 0ull;
-        tm.sync();
-#pragma unroll
-        for (int u = 0; u < NEAR_PER; ++u)
-            if (c[u] >= 0) atomicOr(&bm[(c[u] - cmin) >> 6], 1ull << ((c[u] - cmin) & 63));
-        tm.sync();
-        tm.exclusive_scan(nw, [&](int q) { return (int)__popcll(bm[q]); }, [&](int q, int x) { wpre[q] = x; });
-        tm.sync();
-        const int nU = __builtin_amdgcn_readfirstlane(wpre[nw - 1] + (int)__popcll(bm[nw - 1]));
-        if (nU > NEAR_UMAX) continue;
-        for (int q = lane; q < R * nU; q += 64) uv[q] = 0.0;
-        tm.sync();
-#pragma unroll
-        for (int u = 0; u < NEAR_PER; ++u) {
-            if (c[u] < 0) continue;
-            const int j = A0 + lane + 64 * u, r = (R > 1 && j >= b1) + (R > 2 && j >= b2);
-            const int d = c[u] - cmin;
-            const int rk = wpre[d >> 6] + (int)__popcll(bm[d >> 6] & ((1ull << (d & 63)) - 1));
-            atomicAdd(&uv[r * nU + rk], v[u]);  // (duplicate columns in a row: summed, as their products)
-            p.ucol[A0 + rk] = c[u];             // (the rows that share a column write it alike)
-        }
-        tm.sync();
-        for (int q = lane; q < R * nU; q += 64) p.uval[3LL * A0 + q] = uv[q];
-        if (lane == 0) {
-            p.gna[h] = nU;
-            p.grp[h] = (unsigned char)(R | GRP_NEAR);
-        }
-        if (lane > 0 && lane < R) p.grp[h + lane] = (unsigned char)(GRP_CONT | lane);
-    }
 }
 
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
@@ -2313,7 +2344,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                int* __restrict__ list, Stats* __restrict__ stats,
                                                int dense_span_max, Published* pub, int seq, int tiny_ok,
                                                const unsigned long long* __restrict__ blkflop, int nflop, int nft,
-                                               long long* __restrict__ tslot, SpecPlan sp) {
+                                               long long* __restrict__ tslot) {
     constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
     static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
@@ -2461,24 +2492,6 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     append_block_rows<NUM_NB, PER>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
     if (pub) {
-        if (sp.out) {  // launch-ahead: do this call's bins fit the queued launches?  (SpecPlan)
-            if (threadIdx.x == 0) {
-                auto ld = [&](const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-                const long long nnzC =
-                    __hip_atomic_load(&stats->nnzC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                bool ok = ld(&stats->err) == 0 && nnzC <= sp.cap && ld(&stats->num_count[NUM_GLOBAL]) == 0;
-                for (int b = 1; b < NUM_NB; ++b) {
-                    const int c = ld(&stats->num_count[b]);
-                    sp.out[1 + b] = c;
-                    if (c > 0 && !((sp.mask >> b) & 1)) ok = false;
-                }
-                if (ld(&stats->num_count[NUM_B256]) > 0 && BLOCK_HDR + ld(&stats->num_block_need[0]) > sp.lds[0]) ok = false;
-                if (ld(&stats->num_count[NUM_B1024]) > 0 && BLOCK_HDR + ld(&stats->num_block_need[1]) > sp.lds[1]) ok = false;
-                sp.out[0] = ok;
-                __hip_atomic_store(&stats->spec_ok, (int)ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
-        }
         publish_stats(stats, pub, seq);
         // the host has its copy: leave the device Stats zeroed for the next call (nothing
         // after this kernel reads them), which saves that call a memset launch
@@ -2515,23 +2528,11 @@ struct NumArgs {
     int mc_list, mc_stride;  // row cache: tile-list cap, words per row
     int* cursor;             // this launch's row cursors (block queue, guided / queued wave walks)
     SpillLists sp;           // tile lists of rows past the row cache's cap (symbolic -> numeric)
-    int qall;                // guided bins: every row from the cursor (few rows a wave; < 0: from count)
-    int bin;                 // the launch's numeric bin
-    const int* spec;         // launch-ahead: verdict and counts (SpecPlan), else nullptr
+    int qall;                // guided bins: every row from the cursor (few rows a wave)
     const int* ucol;         // near groups' union rows (GRP_NEAR; see Work)
     const double* uval;
     const int* gna;
 };
-
-// Launch-ahead launches take their count from k_scan's hand-over; false: the plan did not
-// fit this call (the host launches again for the true counts), the kernel returns at once.
-__device__ __forceinline__ bool spec_take(NumArgs& a) {
-    if (!a.spec) return true;
-    if (!a.spec[0]) return false;
-    a.count = a.spec[1 + a.bin];
-    if (a.qall < 0) a.qall = a.count <= MHS_DYN16_MAX;
-    return true;
-}
 
 template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
 __device__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, int span, int t,
@@ -3078,23 +3079,19 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_GRP) void k_num_wave(NumA
 #else
 __global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
 #endif
-    if (!spec_take(a)) return;
     num_wave_rows<BYTES, GROUPED, HASH>(a);
 }
 template <int BYTES>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(BYTES > NUM_WS_BYTES ? MHS_WPE_HASH16 : MHS_WPE_HASH) void k_num_wave_hash(NumArgs a) {
-    if (!spec_take(a)) return;
     num_wave_rows<BYTES, false, true>(a);
 }
 template <int BYTES>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_DIRECT) void k_num_wave_direct(NumArgs a) {
-    if (!spec_take(a)) return;
     num_wave_rows<BYTES, false, false>(a);
 }
 
 template <int T, bool GLOBALMEM>
 __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
-    if (!spec_take(a)) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BlockTeam<T, GLOBALMEM> tm{(long long*)smem};
     char* reg = GLOBALMEM ? (a.gscratch + (long long)blockIdx.x * a.gbytes) : (smem + BLOCK_HDR);
@@ -3162,7 +3159,6 @@ struct TinyArgs {
     long long* tslot;
     long long sbase;
     int blk0[TINY_SYM_NC + 1];  // slots: class c takes blocks [blk0[c], blk0[c+1]) (sized on the host)
-    const int* spec;            // numeric launch-ahead: verdict and counts (SpecPlan), else nullptr
 };
 
 template <int W, int K, bool NUMERIC>
@@ -3173,7 +3169,7 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
     const int tb = lane & ~(W - 1);  // the team's first lane
     const unsigned long long tmask = W == 64 ? ~0ull : (((1ull << (W & 63)) - 1) << tb);
     const unsigned long long below = tmask & lanemask_lt();
-    const int count = a.spec ? a.spec[1 + a.bin] : a.count >= 0 ? a.count : a.stats->sym_count[a.bin];
+    const int count = a.count >= 0 ? a.count : a.stats->sym_count[a.bin];
     const bool slots = NUMERIC && a.sc_col != nullptr;  // numeric-first: into value slots
     const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W), bid, nb);
     extern __shared__ __attribute__((aligned(16))) char tiny_smem[];
@@ -3306,7 +3302,6 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
 
 template <int W, int K>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_TINY) void k_tiny_num(TinyArgs a) {
-    if (a.spec && !a.spec[0]) return;
     tiny_rows<W, K, true>(a, (int)blockIdx.x, (int)gridDim.x);
 }
 
@@ -3319,7 +3314,6 @@ struct TinyFused {
     int blk0[5];
 };
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(8) void k_tiny_num_small(TinyArgs a, TinyFused f) {
-    if (a.spec && !a.spec[0]) return;
     int k = 0;
     while (k + 1 < f.nclass && (int)blockIdx.x >= f.blk0[k + 1]) ++k;
     const int bid = (int)blockIdx.x - f.blk0[k], nb = f.blk0[k + 1] - f.blk0[k];
@@ -3494,7 +3488,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin)
+#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr)
     switch (G) {
     case 2: MHS_ANALYZE(2); break;
     case 4: MHS_ANALYZE(4); break;
@@ -3514,7 +3508,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
 
 void launch_bin_list(const Csr& A, const Work& w, hipStream_t s) {
     const unsigned char* nb = w.nft ? w.nft_bin : nullptr;
-    const NearCand nc{A.ptr, A.col, w.rlo, w.rhi, (w.groups && !nb) ? w.near_list : nullptr};
+    const NearCand nc{w.nsig, (w.groups && !nb) ? w.near_list : nullptr};
     if (scan_per(A.M) == 4)
         hipLaunchKernelGGL(k_bin_list<4>, dim3((A.M + 4095) / 4096), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
                            w.groups, w.bin_list, nb, w.stats, nc);
@@ -3523,27 +3517,11 @@ void launch_bin_list(const Csr& A, const Work& w, hipStream_t s) {
                            w.groups, w.bin_list, nb, w.stats, nc);
 }
 
+static NearArgs near_args(const Csr& A, const Work& w, const int* Cptr);  // (with the symbolic launchers)
+
 void launch_near(const Csr& A, const Work& w, const int* Cptr, hipStream_t s) {
-    if (A.M <= 1 || !w.near_list || !w.groups || w.nft) return;
-    NearArgs p{};
-    p.Aptr = A.ptr;
-    p.Acol = A.col;
-    p.Aval = A.val;
-    p.Cptr = Cptr;
-    p.ctiles = w.ctiles;
-    p.rlo = w.rlo;
-    p.rhi = w.rhi;
-    p.rflop = w.rflop;
-    p.rtflop = w.rtflop;
-    p.mcache = w.mcache;
-    p.mc_list = w.mc_list;
-    p.mc_stride = mc_stride(w.mc_list);
-    p.list = w.near_list;
-    p.stats = w.stats;
-    p.grp = w.grp;
-    p.ucol = w.ucol;
-    p.uval = w.uval;
-    p.gna = w.gna;
+    const NearArgs p = near_args(A, w, Cptr);
+    if (!p.list) return;
     // a persistent grid over the device-side candidate count (none: the waves return at once)
     const int cap = (A.M / 3 + WPB - 1) / WPB;
     hipLaunchKernelGGL(k_near, dim3(round8(cap, MHS_NEAR_GRID)), dim3(256), 0, s, p);
@@ -3684,22 +3662,47 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
 
 // The rare bins (10 KiB waves, 32 KiB and 157 KiB block tables, global memory): one
 // persistent launch that reads the bins' sizes on the device.
-void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s) {
+static NearArgs near_args(const Csr& A, const Work& w, const int* Cptr) {
+    NearArgs p{};
+    if (A.M <= 1 || !w.near_list || !w.groups || w.nft) return p;  // p.list == nullptr: none
+    p.Aptr = A.ptr;
+    p.Acol = A.col;
+    p.Aval = A.val;
+    p.Cptr = Cptr;
+    p.ctiles = w.ctiles;
+    p.rlo = w.rlo;
+    p.rhi = w.rhi;
+    p.rflop = w.rflop;
+    p.rtflop = w.rtflop;
+    p.mcache = w.mcache;
+    p.mc_list = w.mc_list;
+    p.mc_stride = mc_stride(w.mc_list);
+    p.list = w.near_list;
+    p.stats = w.stats;
+    p.grp = w.grp;
+    p.ucol = w.ucol;
+    p.uval = w.uval;
+    p.gna = w.gna;
+    return p;
+}
+
+void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, bool with_near) {
     if (M <= 0) return;
     SymArgs a = sym_args(A, w, M, N, Cptr);
-    hipLaunchKernelGGL(k_sym_rare, dim3(256), dim3(1024), LDS_MAX - 1024, s, a);
+    const NearArgs np = with_near ? near_args(A, w, Cptr) : NearArgs{};
+    hipLaunchKernelGGL(k_sym_rare, dim3(256), dim3(1024), LDS_MAX - 1024, s, a, np);
     a.bin = SYM_B256;
     hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, MHS_SYM_B256_GRID)), dim3(256), SYM_B256_BYTES, s, a);
 }
 
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
-                          Published* pub, int seq, const SpecPlan& sp) {
+                          Published* pub, int seq) {
     // the state words were zeroed by k_analyze (SCAN_ITEMS-row blocks: enough for either width)
     const int per = scan_per(M), nb = (M + 1 + 1024 * per - 1) / (1024 * per);
 #define MHS_SCAN(P)                                                                                                \
     hipLaunchKernelGGL(k_scan<P>, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop,  \
                        w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
-                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, sp)
+                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot)
     if (per == 4) MHS_SCAN(4);
     else MHS_SCAN(1);
 #undef MHS_SCAN
@@ -3727,17 +3730,8 @@ int numeric_launches(const Stats& h) {
 // launches are dealt round-robin over them (launch i on ss[(i + 1) % nss], so the last,
 // bulk wave bins tend to stay on ss[0]): one bin's tail overlaps the next bin's bulk (the
 // reference runs its bins on 12 streams, src/Tool.cu:6-10).  Returns the mask of streams used.
-void numeric_spec_plan(const Stats& h, SpecPlan& sp) {
-    sp.mask = 0;
-    for (int b = 1; b < NUM_NB; ++b)
-        if (h.num_count[b] > 0) sp.mask |= 1 << b;
-    sp.lds[0] = block_lds(h.num_block_need[0], NUM_B256_BYTES);  // (as launch_numeric sizes them)
-    sp.lds[1] = block_lds(h.num_block_need[1], LDS_MAX - 1024);
-}
-
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
-                   double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max,
-                   const int* spec) {
+                   double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max) {
     int nl = 0, used = 0;
     auto next_stream = [&]() {
         const int k = nss > 1 ? (nl + 1) % nss : 0;
@@ -3772,7 +3766,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     a.grp = w.grp;
     a.cursor = w.cursors;
     a.sp = w.spill;
-    a.spec = spec;
     a.ucol = w.ucol;
     a.uval = w.uval;
     a.gna = w.gna;
@@ -3814,7 +3807,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     // Largest bins first so the long rows start early.
     if (h.num_count[NUM_GLOBAL] > 0) {
         const int count = a.count = h.num_count[NUM_GLOBAL];
-        a.bin = NUM_GLOBAL;
         a.list = w.bin_list + (long long)(NUM_GLOBAL - 1) * A.M;
         a.cursor = w.cursors + NUM_GLOBAL * 8 * CURSOR_STRIDE;
         a.gbytes = align16(h.num_global_need);
@@ -3824,7 +3816,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_B1024] > 0) {
         const int count = a.count = h.num_count[NUM_B1024];
-        a.bin = NUM_B1024;
         a.list = w.bin_list + (long long)(NUM_B1024 - 1) * A.M;
         a.cursor = w.cursors + NUM_B1024 * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3833,7 +3824,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_B256] > 0) {
         const int count = a.count = h.num_count[NUM_B256];
-        a.bin = NUM_B256;
         a.list = w.bin_list + (long long)(NUM_B256 - 1) * A.M;
         a.cursor = w.cursors + NUM_B256 * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3842,10 +3832,9 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_W16H] > 0) {
         const int count = a.count = h.num_count[NUM_W16H];
-        a.bin = NUM_W16H;
         a.list = w.bin_list + (long long)(NUM_W16H - 1) * A.M;
         a.cursor = w.cursors + NUM_W16H * 8 * CURSOR_STRIDE;
-        a.qall = spec ? -1 : count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
+        a.qall = count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
         s = next_stream();
         hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_W16H_GRID)),
                            dim3(256), WPB * NUM_W16_BYTES, s, a);
@@ -3853,7 +3842,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_WSH] > 0) {
         const int count = a.count = h.num_count[NUM_WSH];
-        a.bin = NUM_WSH;
         a.list = w.bin_list + (long long)(NUM_WSH - 1) * A.M;
         a.cursor = w.cursors + NUM_WSH * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3862,7 +3850,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_W16] > 0) {
         const int count = a.count = h.num_count[NUM_W16];
-        a.bin = NUM_W16;
         a.list = w.bin_list + (long long)(NUM_W16 - 1) * A.M;
         a.cursor = w.cursors + NUM_W16 * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3882,7 +3869,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         t.Ccol = Ccol;
         t.Cval = Cval;
         t.rlo = w.rlo;
-        t.spec = spec;
         for (int c = TINY_NC - 1; c >= 4; --c) {  // 64-lane classes: kernels of their own (registers)
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;
@@ -3913,7 +3899,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_W16G] > 0) {
         const int count = a.count = h.num_count[NUM_W16G];
-        a.bin = NUM_W16G;
         a.list = w.bin_list + (long long)(NUM_W16G - 1) * A.M;
         a.cursor = w.cursors + NUM_W16G * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3922,7 +3907,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_WSG] > 0) {
         const int count = a.count = h.num_count[NUM_WSG];
-        a.bin = NUM_WSG;
         a.list = w.bin_list + (long long)(NUM_WSG - 1) * A.M;
         a.cursor = w.cursors + NUM_WSG * 8 * CURSOR_STRIDE;
         s = next_stream();
@@ -3931,7 +3915,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_WS] > 0) {
         const int count = a.count = h.num_count[NUM_WS];
-        a.bin = NUM_WS;
         a.list = w.bin_list + (long long)(NUM_WS - 1) * A.M;
         a.cursor = w.cursors + NUM_WS * 8 * CURSOR_STRIDE;
         s = next_stream();

@@ -26,7 +26,6 @@ MHS_OPT_SYNC = 1
 MHS_OPT_NUMERIC_EVENTS = 2
 MHS_OPT_MEM_BUDGET = 3
 MHS_OPT_TINY_FIRST_ROWS = 4
-MHS_OPT_LAUNCH_AHEAD = 5
 
 STATUS_NAMES = {0: "MHS_OK", 1: "MHS_ERR_HIP", 2: "MHS_ERR_OOM", 3: "MHS_ERR_INVALID",
                 4: "MHS_ERR_OVERFLOW", 5: "MHS_ERR_IO"}
@@ -127,8 +126,6 @@ def lib() -> ctypes.CDLL:
     L.mhs_probe_conflicts.restype = c_int
     L.mhs_ctx_chunked_calls.argtypes = [c_void_p]
     L.mhs_ctx_chunked_calls.restype = ctypes.c_longlong
-    L.mhs_ctx_launch_ahead_calls.argtypes = [c_void_p, c_int]
-    L.mhs_ctx_launch_ahead_calls.restype = ctypes.c_longlong
     _lib = L
     return L
 

@@ -82,11 +82,6 @@ class Tool:
         """Calls that ran row-chunked (the out-of-memory fallback)."""
         return int(L.lib().mhs_ctx_chunked_calls(self.ctx))
 
-    def launch_ahead_calls(self):
-        """(hits, misses) of the launch-ahead numeric (MHS_OPT_LAUNCH_AHEAD)."""
-        return (int(L.lib().mhs_ctx_launch_ahead_calls(self.ctx, 0)),
-                int(L.lib().mhs_ctx_launch_ahead_calls(self.ctx, 1)))
-
     def allocate(self, B=None, C=None):  # src/Tool.cu:4 -- workspace grows on demand
         return None
 

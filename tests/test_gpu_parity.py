@@ -628,56 +628,3 @@ def test_numeric_first_tiny_rows(tool, slots, monkeypatch):
     finally:
         t2.close()
 
-
-def _same_lengths_scattered(ptr, N, seed):
-    """Columns drawn anew (sorted, unique, anywhere in [0, N)) for rows of the lengths in ptr."""
-    rng = np.random.default_rng(seed)
-    cols = [np.sort(rng.choice(N, int(ptr[i + 1] - ptr[i]), replace=False)) for i in range(len(ptr) - 1)]
-    return np.concatenate(cols).astype(np.int32)
-
-
-def test_launch_ahead_numeric(tool):
-    """Launch-ahead (MHS_OPT_LAUNCH_AHEAD, SpecPlan): calls without a timing struct on the
-    operands of the last call queue its numeric launches behind the row_ptr scan.  Every
-    product must match the oracle whether the queued plan fits (same structure, new
-    values: hit) or not (same arrays rewritten in place with scattered columns: more C
-    entries and hash bins the plan never launched -- miss, launched again)."""
-    from mhspgemm import _lib as L
-    A = synth.fem_grid(10, 10, 8)  # banded: direct / dense / grouped bins
-    A.H2D(tool.device)
-
-    def run_and_check(p, c, v):
-        C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
-        gp, gc, gv = C.to_host()
-        C.release()
-        Cp, Ci, Cv = orc.spgemm(p, c, v, p, c, v, A.N)
-        assert np.array_equal(gp, Cp) and np.array_equal(gc, Ci)
-        assert mhspgemm.compare_tol(Cp, Ci, Cv, gp, gc, gv, RTOL, ATOL)[0]
-
-    h0, m0 = tool.launch_ahead_calls()
-    mhspgemm.spgemm(tool, A, A)[0].release()  # timed: no launch-ahead, leaves the plan
-    for _ in range(3):
-        run_and_check(A.ptr, A.col, A.val)
-    h1, m1 = tool.launch_ahead_calls()
-    assert (h1 - h0, m1 - m0) == (3, 0)
-    # same values array rewritten: the plan fits, the new values must come out
-    v2 = A.val * 1.5 + 0.25
-    A.d_val.copy_(__import__("torch").from_numpy(v2))
-    run_and_check(A.ptr, A.col, v2)
-    h2, m2 = tool.launch_ahead_calls()
-    assert (h2 - h1, m2 - m1) == (1, 0)
-    # columns rewritten in place (same pointers, same sizes): the plan does not fit
-    c3 = _same_lengths_scattered(A.ptr, A.N, 5)
-    A.d_col.copy_(__import__("torch").from_numpy(c3))
-    run_and_check(A.ptr, c3, v2)
-    h3, m3 = tool.launch_ahead_calls()
-    assert (h3 - h2, m3 - m2) == (0, 1)
-    run_and_check(A.ptr, c3, v2)  # ... and the next call runs ahead on the new plan
-    assert tool.launch_ahead_calls()[0] == h3 + 1
-    # off: no launch-ahead
-    tool.set_option(L.MHS_OPT_LAUNCH_AHEAD, 0)
-    try:
-        run_and_check(A.ptr, c3, v2)
-        assert tool.launch_ahead_calls() == (h3 + 1, m3)
-    finally:
-        tool.set_option(L.MHS_OPT_LAUNCH_AHEAD, 1)

@@ -4,6 +4,5 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 2
 tail -2 gpurun_out/r03s_pytest.log
 bash tools/r02_ab.sh r03s_near "base base@MHS_NO_NEAR=1" "cant-perturbed cant pwtk hood shipsec1" 5 || exit 1
 mkdir -p gpurun_out/r03s_la
-for r in 1 2; do for la in 0 1; do MHS_LAUNCH_AHEAD=$la timeout -k 10 300 python tools/la_sync.py cant cop20k_A mac_econ_fwd500 scircuit rma10 --reps 7 | tee -a gpurun_out/r03s_la/la_sync.jsonl || exit 1; done; done
 bash tools/r02_ab.sh r03s_scan "base scan4" "cant cop20k_A mac_econ_fwd500 scircuit rma10 pdb1HYS" 5 || exit 1
 bash tools/r02_ab.sh r03s_mc "base base@MHS_NO_MCACHE=1" "cage15 webbase-1M" 3 || exit 1
