@@ -42,6 +42,7 @@ struct mhs_ctx {
     bool sync = true;      // MHS_OPT_SYNC
     bool groups = true;     // row groups (MHS_NO_GROUPS=1: every row alone)
     bool near = true;       // near row groups (GRP_NEAR; MHS_NO_NEAR=1: off)
+    bool split = true;      // block bins split by LDS need (MHS_NO_SPLIT=1: off)
     // MHS_OPT_NUMERIC_EVENTS: ring of (start, end) events around the numeric phase
     std::vector<hipEvent_t> nev;
     long long ncalls = 0;
@@ -166,7 +167,7 @@ void pool_put(mhs_ctx* ctx, void* p) {
 
 struct Layout {
     size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, asame, grp, bin_list, scan_part, mcache,
-        stats, blkflop, spill_mask, spill_key, lofs, tslot, nft_bin, near_list, nsig, ucol, uval, gna, total;
+        stats, blkflop, spill_mask, spill_key, lofs, tslot, nft_bin, near_list, nsig, ucol, gna, bx_col, bx_val, split_list, total;
     bool near;
     long long spill_cap;
 };
@@ -207,13 +208,15 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     L.lofs = take((size_t)M * 4);
     L.tslot = take((size_t)M * 8);
     L.nft_bin = take((size_t)M);
+    L.split_list = take((size_t)M * 4);
     L.near = near;
     if (near) {  // near row groups: candidate list, union rows (see Work)
         L.near_list = take((size_t)M * 4);
         L.nsig = take((size_t)M * 4);
         L.ucol = take((size_t)nnzA * 4);
-        L.uval = take((size_t)nnzA * 24);
         L.gna = take((size_t)M * 4);
+        L.bx_col = take((size_t)(nnzB + 3 * nnzA) * 4);  // B's arrays + the union rows (see Work)
+        L.bx_val = take((size_t)(nnzB + 3 * nnzA) * 8);
     }
     L.total = o;
     return L;
@@ -253,7 +256,7 @@ hipError_t alloc_c(mhs_ctx* ctx, mhs_csr* out, long long nnz) {
 }
 
 // The call's Work over the workspace laid out by `L` (rows of this pass: M).
-Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, int Bn, int mc_list) {
+Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, long long nnzB, int Bn, int mc_list) {
     Work w{};
     w.btcol = (int*)(ctx->ws + L.btcol);
     w.btmask = (unsigned long long*)(ctx->ws + L.btmask);
@@ -283,11 +286,15 @@ Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, int Bn, int
     w.spill.top = w.cursors + SPILL_CURSOR_SLOT * 8 * CURSOR_STRIDE;  // zeroed with the cursors
     w.spill.cap = L.spill_cap;
     w.tslot = (long long*)(ctx->ws + L.tslot);
+    w.split_list = (int*)(ctx->ws + L.split_list);
     if (L.near) {
         w.near_list = (int*)(ctx->ws + L.near_list);
         w.nsig = (unsigned*)(ctx->ws + L.nsig);
         w.ucol = (int*)(ctx->ws + L.ucol);
-        w.uval = (double*)(ctx->ws + L.uval);
+        w.bx_col = (int*)(ctx->ws + L.bx_col);
+        w.bx_val = (double*)(ctx->ws + L.bx_val);
+        w.uval = w.bx_val + nnzB;
+        w.ucolx = w.bx_col + nnzB;
         w.gna = (int*)(ctx->ws + L.gna);
     }
     w.stats = (Stats*)(ctx->ws + L.stats);
@@ -340,6 +347,9 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
     const int nl = numeric_launches(h);
     const int nss = (nl >= 3 && h.flop >= (1ull << 24)) ? std::min(ctx->num_streams, nl) : 1;
+    // block bins split by LDS need only where their two launches can run side by side (on
+    // one stream the hub rows' launch would no longer overlap the others' bulk)
+    const bool split = nss > 1 && ctx->split && launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);
     if (nss > 1) {
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         for (int i = 1; i < nss; ++i) {
@@ -348,7 +358,7 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
         }
     }
     const int used =
-        launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID, ctx->dense_span_max);
+        launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID, ctx->dense_span_max, split);
     MHS_HIP(hipGetLastError());
     for (int i = 1; i < nss; ++i)
         if (used & (1 << i)) {
@@ -433,7 +443,7 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
         MHS_HIP(pool_get(ctx, (void**)&tptr, (size_t)(Mc + 1) * 4));
         for (int c = 0; c < nch && rc == MHS_OK; ++c) {
             const Csr a = view(c);
-            Work w = make_work(ctx, L, a.M, a.nnz, B->N, mc_list);
+            Work w = make_work(ctx, L, a.M, a.nnz, B->nnz, B->N, mc_list);
             rc = front_pass(ctx, a, b, w, tptr, c == 0, h);
             if (rc == MHS_OK && h.err)
                 rc = fail(ctx, (h.err & ERR_OVERFLOW) ? MHS_ERR_OVERFLOW : MHS_ERR_INVALID, err_text(h.err));
@@ -476,7 +486,7 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
     for (int c = 0; c < nch; ++c) {
         const Csr a = view(c);
         const int r0 = c * Mc;
-        Work w = make_work(ctx, L, a.M, a.nnz, B->N, mc_list);
+        Work w = make_work(ctx, L, a.M, a.nnz, B->nnz, B->N, mc_list);
         rc = front_pass(ctx, a, b, w, out.ptr + r0, c == 0, h);
         if (rc == MHS_OK) rc = ensure_gscratch(ctx, w, h);
         if (rc) {
@@ -486,7 +496,7 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
         }
         if (h.nnzC > 0)
             launch_numeric(a, b, w, h, out.ptr + r0, out.col + off, out.val + off, &s, 1, NUM_GLOBAL_GRID,
-                           ctx->dense_span_max);
+                           ctx->dense_span_max, false);
         launch_add_offset(out.ptr + r0, a.M + (c == nch - 1 ? 1 : 0), (int)off, s);
         MHS_HIP(hipGetLastError());
         off += h.nnzC;
@@ -556,6 +566,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_MC_LIST")) ctx->mc_list = atoi(e) < MC_LIST_MIN ? MC_LIST_MIN : atoi(e);
     if (getenv("MHS_NO_GROUPS")) ctx->groups = false;
     if (getenv("MHS_NO_NEAR")) ctx->near = false;
+    if (getenv("MHS_NO_SPLIT")) ctx->split = false;
     if (getenv("MHS_NO_TINY_NUM")) ctx->tiny_num = false;
     if (const char* e = getenv("MHS_NFT_MIN_M")) ctx->nft_min_m = atoll(e);
     if (getenv("MHS_NFT_NO_SLOTS")) ctx->nft_slots = false;
@@ -681,7 +692,8 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         }
         if (e != hipSuccess) return fail_hip(ctx, e, "allocating C.ptr");
     }
-    Work w = make_work(ctx, L, M, A->nnz, B->N, mc_list);
+    Work w = make_work(ctx, L, M, A->nnz, B->nnz, B->N, mc_list);
+    w.near_b = L.near && A->ptr == B->ptr && A->col == B->col && A->val == B->val;
     // device Stats start zeroed: the previous call's k_scan left them so, else a memset
     if (!ctx->stats_zero) MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
     ctx->stats_zero = false;  // until this call's k_scan has published and cleared them
@@ -792,6 +804,12 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         }
     }
     rc = ensure_gscratch(ctx, w, h);
+    // near union runs of B (A*A, near groups verified): B's arrays copied in front of the union rows
+    if (rc == MHS_OK && w.near_b && h.near_verified > 0 && B->nnz > 0) {
+        MHS_HIP(hipMemcpyAsync(w.bx_col, B->col, (size_t)B->nnz * 4, hipMemcpyDeviceToDevice, s));
+        MHS_HIP(hipMemcpyAsync(w.bx_val, B->val, (size_t)B->nnz * 8, hipMemcpyDeviceToDevice, s));
+        w.bx_on = 1;
+    }
     if (rc) {
         mhs_ctx_recycle(ctx, &out);
         (void)hipGetLastError();

@@ -39,6 +39,7 @@ constexpr int CURSOR_STRIDE = 16;  // ints
 constexpr int CURSOR_INTS = CURSOR_SLOTS * 8 * CURSOR_STRIDE;
 constexpr int SPILL_PARTS = 64;        // spill-list bump counters: cursor slots 32..39
 constexpr int SPILL_CURSOR_SLOT = 32;
+constexpr int BLOCK_BIG_SLOT = 28;     // cursors of the block bins' hub-row launches (28: 256, 29: 1024 threads)
 static_assert(SPILL_CURSOR_SLOT * 8 + SPILL_PARTS <= CURSOR_SLOTS * 8, "spill counters fit the cursor area");
 
 // Symbolic bins (by LDS need and tile work).
@@ -95,6 +96,7 @@ enum NumBin : int {
     NUM_W16H,
     NUM_NB
 };
+static_assert(NUM_NB + SYM_NB <= BLOCK_BIG_SLOT && BLOCK_BIG_SLOT + 2 <= SPILL_CURSOR_SLOT, "cursor slots do not overlap");
 // Row groups: rows i-1, i of A with the same column pattern (FEM dofs of one node)
 // have C rows with one pattern.  Maximal runs are broken every RG_BREAK rows and cut
 // into groups of at most RG_MAX rows; grp[head] = R, grp[head + o] = GRP_CONT | o.
@@ -132,6 +134,12 @@ constexpr int STAGE_SUBS = 4;           // block kernels stage up to 4 x 64 A en
 constexpr int BLOCK_HDR = 1024 + STAGE_SUBS * 65 * 16;  // per-block LDS header: reductions, counter, A-entry stage
 constexpr int WAVE_HDR = 16;            // per-wave LDS header
 constexpr int B1024_BYTES = LDS_MAX - BLOCK_HDR - 1024;  // budget of the 1024-thread kernels
+// Block bins split by LDS need: a launch takes the LDS of its largest row, so one hub row of
+// 60 KiB would hold every 12 KiB row of the bin to 2 blocks per CU.  Rows at or below the
+// split run in a launch of their own sized to them (4 blocks of 256 / 2 blocks of 1024
+// threads per CU), the rest in a second launch beside it.
+constexpr int B256_SPLIT = LDS_MAX / 4 - BLOCK_HDR - 2048;
+constexpr int B1024_SPLIT = LDS_MAX / 2 - BLOCK_HDR - 2048;
 
 // One 16-byte tile-table entry: OR of the masks of every B tile that maps to
 // this C tile, the C-row rank of its first column, and the key (hash mode).
@@ -151,11 +159,14 @@ struct Stats {
     int num_count[NBINS];
     int num_global_need;           // max LDS-equivalent bytes of a global numeric row
     int num_block_need[2];         // max LDS bytes of a row in NUM_B256 / NUM_B1024 (launch sizing)
+    int num_block_small_need[2];   // ... of the rows at or below BLOCK_SPLIT[bin] (the small launch)
+    int num_block_big[2];          // rows above BLOCK_SPLIT[bin] (their own launch when both kinds exist)
     int final_done;                // k_scan_final blocks finished (last one publishes)
     unsigned long long an_slots;   // numeric-first probe: the candidates' slot entries,
     unsigned long long an_other;   // rows with products past the tiny classes,
     int an_done;                   // and k_probe_publish blocks finished
     int near_heads;                // near-group candidates listed by k_bin_list (k_near's work)
+    int near_verified;             // ... of which verified (union rows built): B's near union runs
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
 // kernel writes it and then `seq`, the host spins on `seq` instead of a stream sync.
@@ -165,6 +176,9 @@ struct Published {
     int pad[3];
 };
 constexpr int SAME_PATTERN = 0x40000000;  // bmeta.z flag: B row repeats row-1's columns
+// bmeta.w of a verified near group's head (B is A; set by k_scan for the numeric pass, over
+// the lo tile only k_analyze reads): NEAR_HEAD | R << 16 | nU -- see finish_chunk
+constexpr int NEAR_HEAD = (int)0x80000000;
 constexpr int ERR_UNSORTED = 1;
 constexpr int ERR_COL_RANGE = 2;
 constexpr int ERR_ACOL_RANGE = 4;
@@ -347,6 +361,13 @@ struct Work {
     int* ucol;
     double* uval;
     int* gna;
+    int near_b;      // B is A with near groups planned: k_scan marks the verified heads in bmeta
+    // B's arrays extended by the near union rows (nnzB + 3 nnzA entries; uval = bx_val + nnzB,
+    // ucolx = bx_col + nnzB): the numeric value walks read them when bx_on (B is A, groups verified)
+    int* bx_col;
+    double* bx_val;
+    int* ucolx;
+    int bx_on;
     int tiny_num;            // numeric tiny classes allowed (per row: column span <= TINY_NUM_NMAX + 1)
     // numeric-first tiny rows (big M): the symbolic tiny launch sorts them once, in the
     // numeric classes, and sums their values into slots (sc_*); numeric only copies them
@@ -358,6 +379,7 @@ struct Work {
     int* sc_col;
     double* sc_val;
     int* bin_list;           // (NUM_NB-1) * M: bin x's rows at (x-1)*M (symbolic bins, then numeric bins)
+    int* split_list;         // M: the block bins' rows split by LDS need (k_split_bins): B1024's, then B256's
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count
     int* scan_part;    // k_scan's look-back state: one 64-bit word per block (flag | prefix)
@@ -388,9 +410,14 @@ void launch_near(const Csr& A, const Work& w, const int* Cptr, hipStream_t s);
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
                           Published* pub, int seq);
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
-                   int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max);
-// numeric launches a call makes for these bin counts (the 32-lane tiny classes share one)
+                   int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max,
+                   bool split);
+// numeric launches a call makes for these bin counts (the 32-lane tiny classes share one; a
+// split block bin makes two)
 int numeric_launches(const Stats& h);
+// Block bins holding rows on both sides of their LDS split: partition their lists into
+// w.split_list (small rows first, hub rows last) on `s`.  False when no bin splits.
+bool launch_split_bins(const Work& w, const Stats& h, int M, const int* Cptr, hipStream_t s, int dense_span_max);
 size_t sym_global_bytes_per_block(int N);
 // p[0..n) += off (row-chunked products: a chunk's row_ptr rebased to its place in C)
 void launch_add_offset(int* p, int n, int off, hipStream_t s);

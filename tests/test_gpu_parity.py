@@ -168,6 +168,29 @@ def test_cant_perturbed_near_groups(tool):
     assert t.num_bins[6] + t.num_bins[7] > A.M // 5, t.num_bins
 
 
+def _perturbed_fem(nx, ny, nz, drop, seed):
+    A = synth.fem_grid(nx, ny, nz, 3, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    rows = np.repeat(np.arange(A.M, dtype=np.int64), np.diff(A.ptr))
+    keep = (rows == A.col) | (rng.random(A.nnz) >= drop)
+    ptr = np.zeros(A.M + 1, np.int64)
+    np.cumsum(np.bincount(rows[keep], minlength=A.M), out=ptr[1:])
+    return mhspgemm.CSR(A.M, A.N, ptr.astype(np.int32), A.col[keep].copy(), A.val[keep].copy())
+
+
+@pytest.mark.parametrize("drop", [0.01, 0.03, 0.08])
+def test_near_union_runs_square(tool, drop):
+    """A*A with near row groups: B's near groups walk their union rows as runs where the A
+    row holds the whole group (finish_chunk), and as single rows where a drop broke the
+    group in the A row.  The same product with B an unaliased copy of A (no union runs)
+    must agree with the oracle too."""
+    A = _perturbed_fem(7, 6, 24, drop, seed=int(drop * 1000))
+    t = check(tool, A, A)
+    assert t.num_bins[6] + t.num_bins[7] > 0, t.num_bins
+    B = mhspgemm.CSR(A.M, A.N, A.ptr.copy(), A.col.copy(), A.val.copy())
+    check(tool, A, B)
+
+
 def test_fem_dof_runs_square(tool):
     # A*A with dof 1..4 per node: runs of every length up to and past the merge cap
     for dof in (1, 2, 3, 4, 6):
