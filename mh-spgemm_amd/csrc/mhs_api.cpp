@@ -804,7 +804,9 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         }
     }
     rc = ensure_gscratch(ctx, w, h);
-    // near union runs of B (A*A, near groups verified): B's arrays copied in front of the union rows
+    // near union runs of B (A*A, near groups verified): B's arrays copied in front of the union
+    // rows (in the near check instead, for every call with candidates: cant-perturbed-like -1.5 %,
+    // cant-s1-like symbolic +5 % -- candidates, no groups)
     if (rc == MHS_OK && w.near_b && h.near_verified > 0 && B->nnz > 0) {
         MHS_HIP(hipMemcpyAsync(w.bx_col, B->col, (size_t)B->nnz * 4, hipMemcpyDeviceToDevice, s));
         MHS_HIP(hipMemcpyAsync(w.bx_val, B->val, (size_t)B->nnz * 8, hipMemcpyDeviceToDevice, s));

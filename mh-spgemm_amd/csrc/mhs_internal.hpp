@@ -130,16 +130,21 @@ constexpr int NUM_WSG_BYTES = 10240;   // grouped rows: 4 waves x 10 KiB = 40 Ki
 constexpr int NUM_B256_BYTES = 65536;
 constexpr int NUM_B256_WORK = 1 << 22;
 constexpr int LDS_MAX = 163840;         // gfx950: 160 KiB per workgroup (probed on the box)
-constexpr int STAGE_SUBS = 4;           // block kernels stage up to 4 x 64 A entries per barrier
+constexpr int STAGE_SUBS = 4;           // 256-thread block kernels stage 4 x 64 A entries per barrier
+// ... the 1024-thread ones 12 x 64 (hub rows of thousands of short-B-row entries were bound by
+// one Acol -> bmeta round trip per 256 entries and barrier)
+constexpr int STAGE_SUBS_1024 = 12;
 constexpr int BLOCK_HDR = 1024 + STAGE_SUBS * 65 * 16;  // per-block LDS header: reductions, counter, A-entry stage
+constexpr int BLOCK_HDR_1024 = 1024 + STAGE_SUBS_1024 * 65 * 16;
+__host__ __device__ constexpr int block_hdr(int T) { return T >= 1024 ? BLOCK_HDR_1024 : BLOCK_HDR; }
 constexpr int WAVE_HDR = 16;            // per-wave LDS header
-constexpr int B1024_BYTES = LDS_MAX - BLOCK_HDR - 1024;  // budget of the 1024-thread kernels
+constexpr int B1024_BYTES = LDS_MAX - BLOCK_HDR_1024 - 1024;  // budget of the 1024-thread kernels
 // Block bins split by LDS need: a launch takes the LDS of its largest row, so one hub row of
 // 60 KiB would hold every 12 KiB row of the bin to 2 blocks per CU.  Rows at or below the
 // split run in a launch of their own sized to them (4 blocks of 256 / 2 blocks of 1024
 // threads per CU), the rest in a second launch beside it.
 constexpr int B256_SPLIT = LDS_MAX / 4 - BLOCK_HDR - 2048;
-constexpr int B1024_SPLIT = LDS_MAX / 2 - BLOCK_HDR - 2048;
+constexpr int B1024_SPLIT = LDS_MAX / 2 - BLOCK_HDR_1024 - 2048;
 
 // One 16-byte tile-table entry: OR of the masks of every B tile that maps to
 // this C tile, the C-row rank of its first column, and the key (hash mode).

@@ -75,9 +75,6 @@
 #ifndef MHS_AN_GMAX
 #define MHS_AN_GMAX 8  // k_analyze: 8 lanes per row (several rows per wave overlap their load chains)
 #endif
-#ifndef MHS_AN_UNROLL
-#define MHS_AN_UNROLL 1
-#endif
 #ifndef MHS_GRP_UNROLL
 #define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
 #endif
@@ -903,22 +900,44 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         const int ps = row > 0 ? Aptr[row - 1] : 0;
         differ = !(row > 0 && e > s && s - ps == e - s);
         const int dp = s - ps;
-#pragma unroll MHS_AN_UNROLL
-        for (int j = s + gl; j < e; j += G) {
-            const int k = Acol[j];
-            const int kp = Acol[j - dp];  // unconditional: stays in [0, nnz(A)); a guarded load would serialise
-            differ = differ || kp != k;
-            if (j == s) kfirst = k;
-            if (k < 0 || k >= MB) {
-                err = ERR_ACOL_RANGE;
-                bad = true;
-                continue;
+        // the whole-wave walk of a long row (hub rows of power-law matrices: thousands of
+        // entries) takes U entries a lane per round, their loads issued together -- one
+        // Acol -> bmeta round trip per U*64 entries instead of per 64
+        constexpr int U = G == 64 ? 4 : 1;
+        for (int j0 = s + gl; j0 < e; j0 += G * U) {
+            int k[U], kp[U];
+            bool in[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j = j0 + u * G;
+                in[u] = j < e;
+                const int jj = in[u] ? j : j0;  // clamped: a cache hit, not counted
+                k[u] = Acol[jj];
+                kp[u] = Acol[jj - dp];  // unconditional: stays in [0, nnz(A)); a guarded load would serialise
             }
-            const int4 m = bmeta[k];
-            flop += m.y;
-            tflop += meta_ntiles(m);
-            lo = min(lo, m.w);
-            hi = max(hi, bhi[k]);
+            int4 m[U];
+            int h[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int kc = in[u] && k[u] >= 0 && k[u] < MB ? k[u] : 0;  // (row 0: a valid slot, unused)
+                m[u] = bmeta[kc];
+                h[u] = bhi[kc];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!in[u]) continue;
+                differ = differ || kp[u] != k[u];
+                if (j0 + u * G == s) kfirst = k[u];
+                if (k[u] < 0 || k[u] >= MB) {
+                    err = ERR_ACOL_RANGE;
+                    bad = true;
+                    continue;
+                }
+                flop += m[u].y;
+                tflop += meta_ntiles(m[u]);
+                lo = min(lo, m[u].w);
+                hi = max(hi, h[u]);
+            }
         }
     }
 #pragma unroll
@@ -1389,7 +1408,7 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
     // entries were bound by one chunk's load chain per barrier).  Sub-chunk s:
     // stage[s*65] = {visits, longest run, group width}; stage[s*65+1+e] = {B start,
     // length, A index, run length}.
-    constexpr int S = (T / 64) < STAGE_SUBS ? (T / 64) : STAGE_SUBS;
+    constexpr int S = T >= 1024 ? STAGE_SUBS_1024 : (T / 64) < STAGE_SUBS ? (T / 64) : STAGE_SUBS;
     const int wv = threadIdx.x >> 6;
     for (int jr = a0; jr < a1; jr += 64 * S) {
         if (wv < S) {
@@ -1878,7 +1897,7 @@ __global__ __launch_bounds__(T) void k_sym_block(SymArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BlockTeam<T, GLOBALMEM> tm{(long long*)smem};
     TileEntry* E = GLOBALMEM ? (TileEntry*)(a.gscratch + (long long)blockIdx.x * a.gbytes)
-                             : (TileEntry*)(smem + BLOCK_HDR);
+                             : (TileEntry*)(smem + block_hdr(T));
     const int count = a.stats->sym_count[a.bin];
     const int* list = a.list + (long long)(a.bin - 1) * a.M;
     int4* stage = (int4*)(smem + 1024);
@@ -2159,7 +2178,7 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a, NearArgs np) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int4* stage = (int4*)(smem + 1024);
     BlockTeam<1024, false> tm{(long long*)smem};
-    TileEntry* E = (TileEntry*)(smem + BLOCK_HDR);
+    TileEntry* E = (TileEntry*)(smem + BLOCK_HDR_1024);
     __shared__ int qslot;
     // phase 0: near row groups (their rows are k_sym_common's, done before this launch)
     if (np.list) {
@@ -3188,7 +3207,7 @@ template <int T, bool GLOBALMEM>
 __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BlockTeam<T, GLOBALMEM> tm{(long long*)smem};
-    char* reg = GLOBALMEM ? (a.gscratch + (long long)blockIdx.x * a.gbytes) : (smem + BLOCK_HDR);
+    char* reg = GLOBALMEM ? (a.gscratch + (long long)blockIdx.x * a.gbytes) : (smem + block_hdr(T));
     int* counter = (int*)(smem + 128);
     int4* stage = (int4*)(smem + 1024);
     __shared__ int qslot;
@@ -3806,9 +3825,9 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
 
 // Dynamic LDS of a block-kernel launch: the header plus its largest row's tables, in
 // 2 KiB steps, at most the bin's budget.
-static int block_lds(int need, int budget) {
+static int block_lds(int need, int budget, int T) {
     if (need <= 0) return budget;
-    const int b = (BLOCK_HDR + need + 2047) & ~2047;
+    const int b = (block_hdr(T) + need + 2047) & ~2047;
     return b < budget ? b : budget;
 }
 
@@ -3986,7 +4005,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         a.gbytes = align16(h.num_global_need);
         const int g = count < global_grid ? count : global_grid;
         s = next_stream();
-        hipLaunchKernelGGL((k_num_block<1024, true>), dim3(g), dim3(1024), BLOCK_HDR, s, a);
+        hipLaunchKernelGGL((k_num_block<1024, true>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, a);
     }
     // block bins: rows past the bin's LDS split (hub rows) in a launch of their own, so the
     // others run at the occupancy their own tables allow
@@ -4006,10 +4025,10 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         if (split && block_split_on(h, k)) {  // k_split_bins: small rows first, hub rows last
             const int big = h.num_block_big[k];
             const int* l = w.split_list + (k ? 0 : (h.num_count[NUM_B1024] > 0 ? h.num_count[NUM_B1024] : 0));
-            go(l + (count - big), big, block_lds(h.num_block_need[k], budget), big_slot);
-            go(l, count - big, block_lds(h.num_block_small_need[k], budget), bin);
+            go(l + (count - big), big, block_lds(h.num_block_need[k], budget, T), big_slot);
+            go(l, count - big, block_lds(h.num_block_small_need[k], budget, T), bin);
         } else {
-            go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget), bin);
+            go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget, T), bin);
         }
     };
     block_bin(NUM_B1024, 1, 1024, 256, LDS_MAX - 1024, BLOCK_BIG_SLOT + 1);
