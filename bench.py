@@ -31,8 +31,16 @@ One JSON line on rank 0: value = 2*flop / (max over ranks of the time per step).
             under profiles/ and keyed by matrix; null for a matrix never profiled).
             The old B_alg (12 B per product, as if every B gather missed to HBM)
             is kept only as the labelled "gather_equiv_GBps": it is not a bound.
-  cpu_baseline: the oracle (CPU restatement, "port") on the same matrix, all
-            host cores, median of repeats.
+  cpu_baseline: the oracle (CPU restatement, "port") on the same matrix, on the
+            OpenMP threads the process gets (the GPU box grants 16 CPUs per GPU and
+            sets OMP_NUM_THREADS=16, while nproc shows the whole host), median of repeats.
+  configs:  (N = 1) the other BASELINE.json configs' stand-ins timed the same way
+            (webbase-1M, mac_econ_fwd500, scircuit, cop20k_A, cage15, cant-perturbed;
+            the metric's 16matrix.txt set, reference process.sh:21-37, printing
+            src/main.cu:136): ms per step, GFLOPS, numeric ms and the compulsory-bytes
+            fractions of the numeric phase and of the whole step.
+  hbm_peak: (N = 1) measured copy / read / write bandwidth of the box
+            (mhs_hbm_peak) beside the 8 TB/s spec the fractions are priced against.
   cold_call: one call on a fresh context (empty workspace and C pool: every
             hipMalloc inside, as the reference's Tool::allocate + C cudaMalloc,
             src/Tool.cu:4-45, src/main.cu:54-61) beside the pooled steady state.
@@ -65,6 +73,8 @@ NUM_BIN_KERNELS = (["", "k_num_wave_direct<5120>", "k_num_wave_direct<10240>", "
                       else f"k_tiny_num<{w},{k}>" for w, k in TINY_WK]
                    + ["k_num_wave_hash<5120>", "k_num_wave_hash<10240>"])
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# BASELINE.json configs[1..3] beyond the headline (configs[4]'s matrix at 1 GPU) + the perturbed cant
+CONFIG_MATRICES = ["cant", "webbase-1M", "mac_econ_fwd500", "scircuit", "cop20k_A", "cage15", "cant-perturbed"]
 
 
 def b_alg(M, nnzA, flop, nnzC):
@@ -146,8 +156,10 @@ def main():
                     help="default: cant (BASELINE configs[1]) on 1 GPU, cage15 (configs[4], row-sharded) on N > 1")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--gather", action="store_true", help="N>1: also time the gatherv of C to rank 0")
-    ap.add_argument("--exchange", default="halo", choices=["halo", "full"],
-                    help="N>1: B rows moved per step: the referenced rows (halo) or every row block (full allgatherv)")
+    ap.add_argument("--exchange", default="full", choices=["halo", "full"],
+                    help="N>1: B rows moved per step: every row block (full: the north_star's allgatherv, "
+                         "the headline) or only the referenced rows (halo); the other mode is timed beside it")
+    ap.add_argument("--no-configs", action="store_true", help="N=1: skip the configs block")
     args = ap.parse_args()
 
     import torch
@@ -215,28 +227,32 @@ def main():
     gather_ms = None
     if world == 1:
         from mhspgemm import _lib as L
+
+        def time_steps(A, steps, warmup):
+            """Pipelined steps (no per-call host sync; hipEvents around each numeric phase on
+            the launch stream).  Returns (elapsed s, numeric ms list)."""
+            tool.set_option(L.MHS_OPT_SYNC, 0)
+            tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, max(1, steps))
+            for _ in range(warmup):
+                C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
+                C.release()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
+                C.release()
+            barrier()
+            el = time.perf_counter() - t0
+            nms = tool.numeric_ms(steps)
+            tool.set_option(L.MHS_OPT_SYNC, 1)
+            tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, 0)
+            return el, nms
+
         A.H2D(local)
-        # timed steps: calls return once the numeric phase is queued (stream-ordered,
-        # no per-call host sync); hipEvents around each numeric phase on the launch stream
-        tool.set_option(L.MHS_OPT_SYNC, 0)
-        tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, max(1, args.steps))
-        for _ in range(args.warmup):
-            C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
-            nnzC = C.nnz
-            C.release()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
-            C.release()
-        barrier()
-        elapsed = time.perf_counter() - t0
+        elapsed, numeric_ms = time_steps(A, args.steps, args.warmup)
         t_max = elapsed
-        numeric_ms = tool.numeric_ms(args.steps)
         # phase breakdown (reference Timing fields): separate, synchronised calls after
         # the timed region
-        tool.set_option(L.MHS_OPT_SYNC, 1)
-        tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, 0)
         for _ in range(5):
             C, t = mhspgemm.spgemm(tool, A, A, timing=True)
             phases.append(t)
@@ -251,6 +267,41 @@ def main():
         cold_tool.close()
         cold = {"t_e2e_ms": round(tc.total_e2e, 4), "gflops": round(2.0 * flop / (tc.total_e2e * 1e-3) / 1e9, 2),
                 "mem_alloc_ms": round(tc.mem_alloc, 4), "Malloc_C_col_val_ms": round(tc.Malloc_C_col_val, 4)}
+        # the metric's set beyond the headline: every other 1-GPU BASELINE config stand-in,
+        # timed exactly like the headline (fewer steps for the big ones)
+        configs = []
+        if not args.no_configs:
+            for m in CONFIG_MATRICES:
+                if m == args.matrix:
+                    continue
+                Am, src_m = synth.load_or_synth(m)
+                fm = mhspgemm.flop_count_np(Am.col, Am.ptr)
+                Am.H2D(local)
+                st = max(3, min(args.steps, 10 if Am.M > 1_000_000 else args.steps))
+                el, nms = time_steps(Am, st, min(args.warmup, 3))
+                C, tm = mhspgemm.spgemm(tool, Am, Am, timing=True)
+                C.release()
+                ms = el / st * 1e3
+                bcm = b_comp(Am.M, Am.nnz, tm.nnzC)
+                avg_n = float(np.mean(nms))
+                configs.append({
+                    "matrix": m, "source": src_m, "rows": Am.M, "nnzA": Am.nnz, "flop": fm, "nnzC": tm.nnzC,
+                    "steps": st, "ms_per_step": round(ms, 4), "gflops": round(2.0 * fm / (ms * 1e-3) / 1e9, 2),
+                    "numeric_ms": round(avg_n, 4), "compulsory_bytes": bcm,
+                    "frac_numeric": round(bcm / (avg_n * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                    "frac_e2e": round(bcm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                    "phases_ms": {k: round(getattr(tm, k), 4) for k in (
+                        "Form_mask_matrix_B", "symbolic_binning", "Calculate_C_nnz", "numeric_binning", "Numeric",
+                        "total_e2e")},
+                })
+                log(f"config {m}: {ms:.3f} ms per step, {configs[-1]['gflops']} GFLOPS")
+                Am.d_release_csr()
+                del Am
+            tool.release()
+        try:
+            hbm = tool.hbm_peak(2 << 30, 10)
+        except Exception as e:  # a diagnostic: never fails the bench
+            hbm = {"error": str(e)}
     else:
         from mhspgemm import distributed as D
         from mhspgemm import _lib as L
@@ -365,7 +416,9 @@ def main():
             "workload": f"{args.matrix}.mtx A*A ({source}), device-resident A -> device-resident sorted C",
             "matrix": args.matrix, "rows": M_glob, "nnzA": nnzA, "flop": flop, "nnzC": nnzC,
             "parallelism": "single GPU" if N_GPUS == 1 else
-                           f"row-sharded x{N_GPUS}, {args.exchange} exchange of B's rows in every step, C distributed"
+                           f"row-sharded x{N_GPUS}, {'full allgatherv (north_star)' if args.exchange == 'full' else 'halo'} "
+                           f"exchange of B's rows in every step (value), {'halo' if args.exchange == 'full' else 'full allgatherv'} "
+                           f"beside it (exchange_alt), C distributed"
                            + (" [gloo rehearsal on one GPU: not a measurement]" if backend == "gloo" else ""),
             "memory": "steady-state steps reuse the context's workspace and pooled C buffers "
                       "(no hipMalloc in a step); cold_call times a fresh context",
@@ -391,6 +444,18 @@ def main():
         }
         assert out["roofline"]["frac"] <= 1.0 and out["roofline"]["e2e_frac"] <= 1.0, out["roofline"]
         out["cold_call"] = cold
+        if "copy_GBps" in hbm:
+            out["roofline"]["peak_measured_copy"] = hbm["copy_GBps"]
+            out["roofline"]["frac_vs_measured_copy"] = round(achieved / hbm["copy_GBps"], 4)
+        out["hbm_peak"] = dict(hbm, spec_GBps=HBM_PEAK_GBPS,
+                               kernels="mhs_hbm_peak: 16 B a lane, 4 in flight, 8 blocks per CU, 2 GiB buffers")
+        if configs:
+            geo = float(np.exp(np.mean([np.log(c["frac_e2e"]) for c in configs + [
+                {"frac_e2e": b_comp(M_glob, nnzA, nnzC) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}]])))
+            out["configs"] = {"matrices": configs, "geomean_frac_e2e_with_headline": round(geo, 4),
+                              "note": "same pipelined steps as value; frac_* = compulsory bytes "
+                                      "8(M+1) + 12 nnz(A) + 12 nnz(C) over the numeric phase / the whole step, "
+                                      "vs the 8 TB/s spec"}
         ph = {k: round(float(np.mean([getattr(p, k) for p in phases])), 4)
               for k in ("mem_alloc", "Form_mask_matrix_B", "symbolic_binning", "Calculate_C_nnz",
                         "numeric_binning", "Malloc_C_col_val", "Numeric", "total_e2e")}
@@ -409,7 +474,9 @@ def main():
                 "sample": f"full {args.matrix} A*A (symbolic+numeric, Gustavson, oracle/), median of {reps} "
                           f"runs of {med*1e3:.1f} ms on {threads} OpenMP threads; 1 thread: "
                           f"{2.0 * flop / one / 1e9:.3f} GFLOPS ({one*1e3:.0f} ms)",
-                "host": {"nproc": nproc, "cpu_model": model, "omp_threads": threads},
+                "host": {"nproc": nproc, "cpu_model": model, "omp_threads": threads,
+                         "cap": "OMP_NUM_THREADS: the GPU box grants 16 CPUs per GPU (harness setting); "
+                                "nproc counts the whole host"},
             }
         else:
             out["cpu_baseline"] = None

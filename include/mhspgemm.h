@@ -177,6 +177,13 @@ int mhs_memcpy(mhs_ctx *ctx, void *dst, const void *src, size_t bytes, int kind)
 int mhs_device_alloc(mhs_ctx *ctx, void **p, size_t bytes);
 int mhs_device_free(mhs_ctx *ctx, void *p);
 
+/* Measured HBM bandwidth of the context's device (a diagnostic beside the 8 TB/s spec that
+ * the roofline fractions are priced against; not on the SpGEMM path): streaming kernels over
+ * two `bytes` buffers (>= 1 MiB; allocated and freed inside), each run `iters` times
+ * between hipEvents.  gbps[0] = copy (read + write bytes), gbps[1] = read, gbps[2] = write,
+ * in GB/s (1e9 B/s).  Synchronous. */
+int mhs_hbm_peak(mhs_ctx *ctx, size_t bytes, int iters, double *gbps);
+
 int mhs_abi_version(void);
 
 #ifdef __cplusplus

@@ -168,11 +168,15 @@ void pool_put(mhs_ctx* ctx, void* p) {
 struct Layout {
     size_t btcol, btmask, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles, sym_bin, asame, grp, bin_list, scan_part, mcache,
         stats, blkflop, spill_mask, spill_key, lofs, tslot, nft_bin, near_list, nsig, ucol, gna, bx_col, bx_val, split_list, total;
-    bool near;
+    bool near, near_b;
+    long long bx_pre;  // B's entries in front of the union rows in bx_* (B is A), else 0
     long long spill_cap;
 };
 
-Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_total = -1, bool near = false) {
+// near: near row groups planned; near_b: B is A (the union rows also serve B's union runs, so
+// B's arrays are copied in front of them -- A != B reserves only the union rows)
+Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_total = -1, bool near = false,
+            bool near_b = false) {
     Layout L{};
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -211,12 +215,14 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     L.split_list = take((size_t)M * 4);
     L.near = near;
     if (near) {  // near row groups: candidate list, union rows (see Work)
+        L.near_b = near_b;
+        L.bx_pre = near_b ? nnzB : 0;
         L.near_list = take((size_t)M * 4);
         L.nsig = take((size_t)M * 4);
         L.ucol = take((size_t)nnzA * 4);
         L.gna = take((size_t)M * 4);
-        L.bx_col = take((size_t)(nnzB + 3 * nnzA) * 4);  // B's arrays + the union rows (see Work)
-        L.bx_val = take((size_t)(nnzB + 3 * nnzA) * 8);
+        if (near_b) L.bx_col = take((size_t)(nnzB + 3 * nnzA) * 4);  // B's arrays + the union rows (see Work)
+        L.bx_val = take((size_t)(L.bx_pre + 3 * nnzA) * 8);
     }
     L.total = o;
     return L;
@@ -291,10 +297,12 @@ Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, long long n
         w.near_list = (int*)(ctx->ws + L.near_list);
         w.nsig = (unsigned*)(ctx->ws + L.nsig);
         w.ucol = (int*)(ctx->ws + L.ucol);
-        w.bx_col = (int*)(ctx->ws + L.bx_col);
         w.bx_val = (double*)(ctx->ws + L.bx_val);
-        w.uval = w.bx_val + nnzB;
-        w.ucolx = w.bx_col + nnzB;
+        w.uval = w.bx_val + L.bx_pre;
+        if (L.near_b) {  // B is A: its union runs read bx_*
+            w.bx_col = (int*)(ctx->ws + L.bx_col);
+            w.ucolx = w.bx_col + nnzB;
+        }
         w.gna = (int*)(ctx->ws + L.gna);
     }
     w.stats = (Stats*)(ctx->ws + L.stats);
@@ -415,11 +423,10 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
         const int est = (int)((long long)A->nnz * (r1 - r0) / (M > 0 ? M : 1));
         return Csr{r1 - r0, A->N, est, A->ptr + r0, A->col, A->val};
     };
-    // the workspace for chunks of Mc rows (Mc halved from `from` until it fits)
-    auto fit_workspace = [&](int from) {
-        for (Mc = from;;) {
-            if (Mc <= 1) return fail(ctx, MHS_ERR_OOM, "a one-row workspace does not fit the device");
-            Mc = (Mc + 1) / 2;
+    // the workspace for chunks of Mc rows: `first` rows, then halved until it fits (a one-row
+    // workspace is tried before the call gives up)
+    auto fit_workspace = [&](int first) {
+        for (Mc = first;; Mc = (Mc + 1) / 2) {
             if (ctx->ws) (void)hipFree(ctx->ws);
             ctx->ws = nullptr;
             ctx->ws_bytes = 0;
@@ -429,9 +436,10 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
             const int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
             if (rc != MHS_ERR_OOM) return rc;
             (void)hipGetLastError();
+            if (Mc <= 1) return fail(ctx, MHS_ERR_OOM, "a one-row workspace does not fit the device");
         }
     };
-    int rc = fit_workspace(M);
+    int rc = fit_workspace((M + 1) / 2);  // (the whole-M workspace has just failed)
     if (rc) return rc;
     // pass 1: counts
     int nch = (M + Mc - 1) / Mc;
@@ -473,7 +481,7 @@ int spgemm_chunked(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C,
         }
     }
     ctx->c_held = (size_t)(M + 1) * 4 + (size_t)total * 12;
-    rc = fit_workspace(2 * Mc1 - 1);  // (starts at Mc1: the first halving gives it back)
+    rc = fit_workspace(Mc1);  // (pass 1 fitted Mc1 rows alone; C now sits beside it)
     ctx->c_held = 0;
     if (rc) {
         mhs_csr_free(&out);
@@ -677,10 +685,17 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     const bool probe = ctx->tiny_num && ctx->nft_min_m >= 0 && M >= ctx->nft_min_m && M > 0;
     // near row groups: with the row cache (their C patterns are compared there), not with
     // the numeric-first probe (big M), and union rows of at most 3 x 32 M values
-    const bool near = ctx->near && ctx->groups && ctx->use_mcache && !probe && A->nnz <= (1 << 25);
-    const Layout L = plan(M, MB, A->nnz, B->nnz, mc_list, -1, near);
+    bool near = ctx->near && ctx->groups && ctx->use_mcache && !probe && A->nnz <= (1 << 25);
+    const bool same_ab = A->ptr == B->ptr && A->col == B->col && A->val == B->val;
+    Layout L = plan(M, MB, A->nnz, B->nnz, mc_list, -1, near, near && same_ab);
     const char* ws_before = ctx->ws;
     int rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
+    if (rc == MHS_ERR_OOM && near) {  // near groups are an optimisation: drop them before chunking
+        (void)hipGetLastError();
+        near = false;
+        L = plan(M, MB, A->nnz, B->nnz, mc_list, -1, false);
+        rc = ensure(ctx, &ctx->ws, &ctx->ws_bytes, L.total);
+    }
     if (rc == MHS_ERR_OOM && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
     if (rc) return rc;
     if (ctx->ws != ws_before) ctx->stats_zero = false;
@@ -693,7 +708,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         if (e != hipSuccess) return fail_hip(ctx, e, "allocating C.ptr");
     }
     Work w = make_work(ctx, L, M, A->nnz, B->nnz, B->N, mc_list);
-    w.near_b = L.near && A->ptr == B->ptr && A->col == B->col && A->val == B->val;
+    w.near_b = L.near && same_ab;
     // device Stats start zeroed: the previous call's k_scan left them so, else a memset
     if (!ctx->stats_zero) MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
     ctx->stats_zero = false;  // until this call's k_scan has published and cleared them

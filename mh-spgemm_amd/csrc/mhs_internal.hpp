@@ -172,6 +172,7 @@ struct Stats {
     int an_done;                   // and k_probe_publish blocks finished
     int near_heads;                // near-group candidates listed by k_bin_list (k_near's work)
     int near_verified;             // ... of which verified (union rows built): B's near union runs
+    int nonfinite;                 // k_mask_b met an Inf / NaN in B's values (near groups planned): none
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
 // kernel writes it and then `seq`, the host spins on `seq` instead of a stream sync.
@@ -188,6 +189,7 @@ constexpr int ERR_UNSORTED = 1;
 constexpr int ERR_COL_RANGE = 2;
 constexpr int ERR_ACOL_RANGE = 4;
 constexpr int ERR_OVERFLOW = 8;
+constexpr int ERR_NONFINITE = 16;  // (k_mask_b's lane flag only: Stats::nonfinite, never an error)
 
 __host__ __device__ inline int next_pow2(int x) {
     int p = 1;

@@ -724,7 +724,7 @@ template <int G>
 __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* __restrict__ ptr,
                                          const int* __restrict__ col, int* __restrict__ btcol,
                                          unsigned long long* __restrict__ btmask, int4* __restrict__ bmeta,
-                                         int* __restrict__ bhi, int& err) {
+                                         int* __restrict__ bhi, int& err, const double* __restrict__ vcheck) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
@@ -758,6 +758,7 @@ __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* 
         const bool head = in && tile != ptile;
         if (in && c < pc) err |= ERR_UNSORTED;
         if (in && (c < 0 || c >= N)) err |= ERR_COL_RANGE;
+        if (vcheck && in && !__builtin_isfinite(vcheck[j])) err |= ERR_NONFINITE;
         // next entry's column: within the chunk from the neighbour lane, at the
         // chunk edge from memory
         const int dn = __shfl_down(c, 1, G);
@@ -808,7 +809,7 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
                                                 const int* __restrict__ col, int* __restrict__ btcol,
                                                 unsigned long long* __restrict__ btmask,
                                                 int4* __restrict__ bmeta, int* __restrict__ bhi,
-                                                Stats* __restrict__ stats) {
+                                                Stats* __restrict__ stats, const double* __restrict__ vcheck) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
@@ -816,18 +817,20 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
     int err = 0;
     bool lng = false;
     if constexpr (G < 64) lng = valid && ptr[row + 1] - ptr[row] > MASK_LONG * G;
-    mask_row<G>(row, valid && !lng, N, ptr, col, btcol, btmask, bmeta, bhi, err);
+    mask_row<G>(row, valid && !lng, N, ptr, col, btcol, btmask, bmeta, bhi, err, vcheck);
     if constexpr (G < 64) {
         for (unsigned long long lb = __ballot(lng && gl == 0); lb; lb &= lb - 1) {
             const int r = __shfl(row, __builtin_ctzll(lb));
-            mask_row<64>(r, true, N, ptr, col, btcol, btmask, bmeta, bhi, err);
+            mask_row<64>(r, true, N, ptr, col, btcol, btmask, bmeta, bhi, err, vcheck);
         }
     }
     if (__any(err != 0)) {
         int werr = err;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) werr |= __shfl_xor(werr, d);
-        if (lane == 0) atomicOr(&stats->err, werr);
+        // a non-finite B value is not an error: it only turns near row groups off (k_bin_list)
+        if (lane == 0 && (werr & ~ERR_NONFINITE)) atomicOr(&stats->err, werr & ~ERR_NONFINITE);
+        if (lane == 0 && (werr & ERR_NONFINITE)) stats->nonfinite = 1;
     }
 }
 
@@ -967,7 +970,8 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         sym_bin[row] = (unsigned char)bin;
         // near row-group signature (k_bin_list links rows whose signatures match: the same
         // C tile span and first A column, both in the small-table wave bin); a collision only
-        // adds a candidate that k_sym_rare's check turns down
+        // adds a candidate that k_sym_rare's check turns down (it compares every row's span,
+        // counts and row-cache words with the head's)
         if (nsig)
             nsig[row] = (bin == SYM_WAVE && nA >= 8 && !bad)
                             ? (((unsigned)lo * 0x9E3779B1u) ^ ((unsigned)hi * 0x85EBCA77u) ^
@@ -2080,8 +2084,10 @@ __device__ void near_groups(const NearArgs& p, char* lds, int gw, int nwaves) {
         const int h = e >> 2, R = e & 3;
         // 1. the rows' scalars, lane r for row h + r
         const bool rl = lane < R;
-        int n = 0, t = 0, tf = 0, fl = 0, a0 = 0, a1 = 0;
+        int n = 0, t = 0, tf = 0, fl = 0, a0 = 0, a1 = 0, rlo_l = 0, rhi_l = 0;
         if (rl) {
+            rlo_l = p.rlo[h + lane];
+            rhi_l = p.rhi[h + lane];
             n = p.Cptr[h + lane];
             t = p.ctiles[h + lane];
             tf = p.rtflop[h + lane];
@@ -2089,8 +2095,9 @@ __device__ void near_groups(const NearArgs& p, char* lds, int gw, int nwaves) {
             a0 = p.Aptr[h + lane];
             a1 = p.Aptr[h + lane + 1];
         }
-        const int lo = __builtin_amdgcn_readfirstlane(p.rlo[h]);
-        const int span = __builtin_amdgcn_readfirstlane(p.rhi[h]) - lo + 1;
+        const int lo = __builtin_amdgcn_readfirstlane(rlo_l);
+        const int hi = __builtin_amdgcn_readfirstlane(rhi_l);
+        const int span = hi - lo + 1;
         // the row cache form of each row's C pattern (1: masks over the span, 2: a tile list)
         const int f = !rl || !sym_direct(span, tf) || tiny_class_sym(fl, a1 - a0) >= 0 ? 0
                       : mcached(span, tf)                                              ? 1
@@ -2102,7 +2109,7 @@ __device__ void near_groups(const NearArgs& p, char* lds, int gw, int nwaves) {
         const int b1 = __shfl(a0, 1), b2 = __shfl(a0, 2);  // rows 1, 2 start (R > 1, > 2)
         const unsigned long long rm = (1ull << R) - 1;
         if (n0 <= 0 || f0 == 0 || !p.mcache || A1 - A0 > 64 * NEAR_PER ||
-            (__ballot(rl && n == n0 && t == t0 && f == f0) & rm) != rm)
+            (__ballot(rl && n == n0 && t == t0 && f == f0 && rlo_l == lo && rhi_l == hi) & rm) != rm)
             continue;
         // 2. the row cache words of rows 1.. against row 0's, and the rows' A entries
         const int words = f0 == 1 ? span : t0;
@@ -2153,7 +2160,7 @@ __device__ void near_groups(const NearArgs& p, char* lds, int gw, int nwaves) {
             const int rk = wpre[d >> 6] + (int)__popcll(bm[d >> 6] & ((1ull << (d & 63)) - 1));
             atomicAdd(&uv[r * nU + rk], v[u]);  // (duplicate columns in a row: summed, as their products)
             p.ucol[A0 + rk] = c[u];             // (the rows that share a column write it alike)
-            p.ucolx[3LL * A0 + rk] = c[u];
+            if (p.ucolx) p.ucolx[3LL * A0 + rk] = c[u];
         }
         tm.sync();
         for (int q = lane; q < R * nU; q += 64) p.uval[3LL * A0 + q] = uv[q];
@@ -2307,6 +2314,9 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
     __shared__ unsigned char lk_s[LK];
     __shared__ int ncand_s, nbase_s;  // the block's near candidates: one counter add per block
     if (threadIdx.x == 0) ncand_s = 0;
+    // a non-finite B value (k_mask_b): no near groups -- their zero-padded products would turn
+    // 0 * Inf into NaN where the reference never forms the product
+    if (nc.list && stats->nonfinite) nc.list = nullptr;
     const long long lbase = (long long)blockIdx.x * (1024 * PER) - RG_BREAK;
     // link of row r to row r-1: 1 = the same A pattern, 2 = a near candidate (see GRP_NEAR;
     // rows of the small-table wave bin only: k_sym_rare checks them after k_sym_common), 0 = none
@@ -3562,8 +3572,14 @@ static int round8(long long x, int cap) {
     return (int)((g + 7) / 8 * 8);
 }
 
+// Must run on every call, even when B is unchanged: it rewrites all of bmeta, and k_scan
+// marks near heads in bmeta.w (over the lo tile) for the numeric pass -- a skipped mask pass
+// would let stale NEAR_HEAD bits reach k_analyze.
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     if (B.M <= 0) return;
+    // near row groups add explicit 0*b / a*0 products: B's values (= A's when B is A) are
+    // checked for Inf / NaN on the way, and a non-finite value turns near groups off
+    const double* vcheck = w.near_list ? B.val : nullptr;
     // about four chunk iterations per row: a wave then holds several rows, whose
     // dependent load chains overlap (measured on gfx950: 64-lane rows were latency-bound)
     const long long avg = B.M > 0 ? B.nnz / B.M : 0;
@@ -3573,12 +3589,12 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     const int rpb = 256 / G;
     const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
     switch (G) {
-    case 2: hipLaunchKernelGGL(k_mask_b<2>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    case 4: hipLaunchKernelGGL(k_mask_b<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    case 32: hipLaunchKernelGGL(k_mask_b<32>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    default: hipLaunchKernelGGL(k_mask_b<64>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    case 2: hipLaunchKernelGGL(k_mask_b<2>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
+    case 4: hipLaunchKernelGGL(k_mask_b<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
+    case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
+    case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
+    case 32: hipLaunchKernelGGL(k_mask_b<32>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
+    default: hipLaunchKernelGGL(k_mask_b<64>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
     }
 }
 
@@ -3796,7 +3812,7 @@ static NearArgs near_args(const Csr& A, const Work& w, const int* Cptr) {
     p.ucol = w.ucol;
     p.uval = w.uval;
     p.gna = w.gna;
-    p.ucolx = w.ucolx;
+    p.ucolx = w.near_b ? w.ucolx : nullptr;  // (B's union runs: B is A)
     p.verified = &w.stats->near_verified;
     return p;
 }

@@ -82,6 +82,14 @@ class Tool:
         """Calls that ran row-chunked (the out-of-memory fallback)."""
         return int(L.lib().mhs_ctx_chunked_calls(self.ctx))
 
+    def hbm_peak(self, nbytes: int = 2 << 30, iters: int = 10) -> dict:
+        """Measured HBM bandwidth of this device (GB/s): copy (read + write bytes), read,
+        write streaming kernels over `nbytes` buffers (mhs_hbm_peak)."""
+        out = (ctypes.c_double * 3)()
+        _check(self.ctx, L.lib().mhs_hbm_peak(self.ctx, nbytes, iters, out), "mhs_hbm_peak")
+        return {"copy_GBps": round(out[0], 1), "read_GBps": round(out[1], 1), "write_GBps": round(out[2], 1),
+                "buffer_bytes": int(nbytes), "iters": int(iters)}
+
     def allocate(self, B=None, C=None):  # src/Tool.cu:4 -- workspace grows on demand
         return None
 

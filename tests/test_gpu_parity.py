@@ -191,6 +191,32 @@ def test_near_union_runs_square(tool, drop):
     check(tool, A, B)
 
 
+def test_near_groups_nonfinite_values(tool):
+    """Near groups and union runs add explicit 0*b / a*0 products, which turn into NaN when
+    b or a is Inf / NaN, where the reference (src/CSR.cu:48-96 compares every entry) never
+    forms the product.  k_mask_b checks B's values (A's, when B is A) and a non-finite
+    value turns near groups off for the call: Inf and NaN land exactly where the oracle has
+    them, A*A and A*B with B an unaliased copy."""
+    A0 = _perturbed_fem(7, 6, 24, 0.03, seed=31)
+    v = A0.val.copy()
+    v[[5, 1000, 2500, 7001]] = np.inf
+    v[777] = -np.inf
+    v[4321] = np.nan
+    A = mhspgemm.CSR(A0.M, A0.N, A0.ptr, A0.col, v)
+    for B in (A, mhspgemm.CSR(A.M, A.N, A.ptr.copy(), A.col.copy(), A.val.copy())):
+        p, c, vv, t = run_gpu(tool, A, B)
+        Cp, Ci, Cv = orc.spgemm(A.ptr, A.col, A.val, B.ptr, B.col, B.val, B.N)
+        assert np.array_equal(p, Cp) and np.array_equal(c, Ci)
+        assert np.array_equal(np.isnan(vv), np.isnan(Cv)), "NaN positions differ"
+        assert np.array_equal(np.isposinf(vv), np.isposinf(Cv)) and np.array_equal(np.isneginf(vv), np.isneginf(Cv))
+        fin = np.isfinite(Cv)
+        assert fin.sum() > len(Cv) // 2
+        assert np.allclose(vv[fin], Cv[fin], rtol=RTOL, atol=ATOL)
+    # the finite product of the same pattern does run near groups (the switch is per call)
+    t = check(tool, A0, A0)
+    assert t.num_bins[6] + t.num_bins[7] > 0, t.num_bins
+
+
 def test_fem_dof_runs_square(tool):
     # A*A with dof 1..4 per node: runs of every length up to and past the merge cap
     for dof in (1, 2, 3, 4, 6):
@@ -543,7 +569,7 @@ def test_oom_row_chunked_fallback(tool):
     A.H2D(tool.device)
     small = mhspgemm.Tool(tool.device)
     try:
-        small.set_option(L.MHS_OPT_MEM_BUDGET, 300)  # MiB: C is 210 MB, the full workspace ~170 MB
+        small.set_option(L.MHS_OPT_MEM_BUDGET, 300)  # MiB: C is 210 MB, the workspace ~170 MB without near groups (~380 MB with them: dropped first)
         C, t = mhspgemm.spgemm(small, A, A)
         p, c, v = C.to_host()
         C.release()
@@ -561,6 +587,26 @@ def test_oom_row_chunked_fallback(tool):
             mhspgemm.spgemm(small, A, A)
         assert e.value.status == 2 and "C itself" in str(e.value)
         assert time.perf_counter() - t0 < 3.0
+    finally:
+        small.close()
+
+
+def test_oom_one_row_chunks(tool, monkeypatch):
+    # when the counting pass only fits one-row chunks, the second pass must try the
+    # one-row workspace beside C too.  A 100 000-tile row-cache slot (1.2 MB a row) makes a
+    # 2-row workspace exceed a 2 MiB budget while a 1-row one fits; C is a few KB.
+    from mhspgemm import _lib as L
+    monkeypatch.setenv("MHS_MC_LIST", "100000")
+    monkeypatch.setenv("MHS_SPILL_CAP", "1024")
+    small = mhspgemm.Tool(tool.device)
+    try:
+        p, c, v = random_csr(24, 40, 3, seed=11)
+        Bp, Bc, Bv = random_csr(40, 30, 2, seed=12)
+        A = mhspgemm.CSR(24, 40, p, c, v)
+        B = mhspgemm.CSR(40, 30, Bp, Bc, Bv)
+        small.set_option(L.MHS_OPT_MEM_BUDGET, 2)
+        t = check(small, A, B)
+        assert small.chunked_calls() == 1 and t.nnzC > 0
     finally:
         small.close()
 

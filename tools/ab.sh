@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of library variants (tools/var/<v>/libmhspgemm.so): sweep lines per matrix, two interleaved rounds.
-# usage: tools/r02_ab.sh <tag> "<variants>" "<matrices>" [reps]
+# usage: tools/ab.sh <tag> "<variants>" "<matrices>" [reps]
 export TMPDIR=/tmp MHS_SYNTH_CACHE=/tmp/mhs_synth
 tag=$1; vs=$2; ms=$3; reps=${4:-7}
 out=gpurun_out/$tag; mkdir -p $out

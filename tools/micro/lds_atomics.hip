@@ -1,6 +1,8 @@
 // LDS throughput microbenchmark (gfx950): cycles per wave-instruction of ds_add_f64 (atomic,
 // distinct addresses per lane), a ds_read_b64 + v_add_f64 + ds_write_b64 read-modify-write,
 // and ds_add_f64 with 4 lanes per address -- one CU-filling launch each, timed with events.
+// build: /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o tools/micro/lds_atomics tools/micro/lds_atomics.hip
+// (the binary is git-ignored; results: profiles/r03/micro_lds_atomics.txt)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 template <int MODE>
