@@ -101,7 +101,7 @@ def pmc_traffic(matrix: str):
         d = json.loads(f.read_text())
         m = d["matrices"][matrix]
         ks = {k: v for k, v in m["kernels"].items()
-              if k.split("::")[-1].startswith(NUMERIC_PREFIXES)}
+              if k.split("::")[-1].startswith(NUMERIC_PREFIXES) and v.get("hbm_bytes_per_call") is not None}
         if not ks:
             return None, None, None
         tot = sum(v["hbm_bytes_per_call"] for v in ks.values())

@@ -29,6 +29,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <functional>
+#include <vector>
 
 #ifndef MHS_ROW_STAMPS
 #define MHS_ROW_STAMPS 0  // 1: tools/diag/stamps*.py builds -- per-row, per-phase s_memtime cycles
@@ -853,13 +855,12 @@ __device__ __forceinline__ int sym_bin_of(int flop, int tflop, int span) {
 // no barrier on the path to the host.
 __device__ void publish_stats(const Stats* stats, Published* pub, int seq) {
     constexpr int NW = (int)(sizeof(Stats) / 4);
-    static_assert(sizeof(Stats) % 4 == 0 && NW <= 64, "Stats is copied one word per lane of wave 0");
+    static_assert(sizeof(Stats) % 4 == 0 && NW <= 1024, "Stats is copied by wave 0, zeroed by one block");
     if (threadIdx.x >= 64) return;
     const int* src = reinterpret_cast<const int*>(stats);
     int* dst = reinterpret_cast<int*>(&pub->stats);
-    if (threadIdx.x < NW)
-        __hip_atomic_store(dst + threadIdx.x,
-                           __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+    for (int i = threadIdx.x; i < NW; i += 64)
+        __hip_atomic_store(dst + i, __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2406,6 +2407,7 @@ __device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t
                                                 int nA, bool tiny_ok) {
     if (R < 2 || n == 0 || (tiny_ok && tiny_class(flop, nA, TINY_NUM_SMALL) >= 0))
         return NUM_NONE;  // tiny rows: one by one
+    if (num_mode(span, t, n, dense_span_max) == NM_HASH) return NUM_NONE;  // (grouped kernels: direct tables only)
     const long long need = num_need_rows(span, t, n, dense_span_max, R);
     if (need <= NUM_WSG_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WSG;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16G;
@@ -2450,7 +2452,13 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     __shared__ long long ws[16];
     __shared__ long long excl_s;
     __shared__ int bid_s;
+    __shared__ unsigned long long bwork_s[NUM_NB];  // the block's products (+ a row overhead) per numeric bin
+    __shared__ int bmax_s[NUM_NB];                  // ... and its heaviest row's
     const int lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x < NUM_NB) {
+        bwork_s[threadIdx.x] = 0ull;
+        bmax_s[threadIdx.x] = 0;
+    }
     // grids of <= 256 blocks (M <= 256K rows) are co-resident (a 1024-thread block with
     // ~1 KiB of LDS fits any CU), so no block can wait on one that never starts: the
     // block index serves, and the ticket's atomic round trip leaves the critical path
@@ -2531,6 +2539,36 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                   tok);
         }
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
+        {  // work estimate of the row's launch (launch_numeric deals launches by it): products
+           // (a group head: the group's), + 64 for the row's fixed steps
+            const int g0 = i < M ? (int)grp[i] : 0;
+            const int gR = (!(g0 & GRP_CONT) && nbin != NUM_NONE) ? ((g0 & GRP_RMASK) > 1 ? (g0 & GRP_RMASK) : 1) : 1;
+            const long long wr = nbin != NUM_NONE ? (long long)rflop[i] * gR : 0;
+            for (unsigned long long todo = __ballot(nbin != NUM_NONE); todo;) {
+                const int b = __builtin_amdgcn_readfirstlane(__shfl(nbin, __builtin_ctzll(todo)));
+                const unsigned long long mine = __ballot(nbin == b);
+                todo &= ~mine;
+                const unsigned long long sw = wave_sum(nbin == b ? (unsigned long long)wr + 64 : 0ull);
+                const int mw = wave_max(nbin == b ? sat_int(wr) : 0);
+                if (lane == 0) {
+                    atomicAdd(&bwork_s[b], sw);
+                    atomicMax(&bmax_s[b], mw);
+                }
+            }
+        }
+        // the grouped wave bins' launches take LDS regions sized to their largest group (a 3-row FEM
+        // group needs ~7 KB of the 10 KiB region: 5 waves per SIMD instead of 4)
+        {
+            int gneed = 0;
+            if (nbin == NUM_WSG || nbin == NUM_W16G) {
+                const int gg = grp[i] & GRP_RMASK;
+                gneed = (int)num_need_rows(rhi[i] - rlo[i] + 1, ctiles[i], v[k], dense_span_max, gg > 1 ? gg : 1) +
+                        WAVE_HDR;
+            }
+            const int gs = wave_max(nbin == NUM_WSG ? gneed : 0), g16 = wave_max(nbin == NUM_W16G ? gneed : 0);
+            if (lane == 0 && gs) atomicMax(&stats->num_wave_need[0], gs);
+            if (lane == 0 && g16) atomicMax(&stats->num_wave_need[1], g16);
+        }
         // the block kernels' launches get the LDS their largest row needs (more blocks per
         // CU than a fixed 64 / 157 KiB when the rows are smaller)
         int need = 0;
@@ -2603,6 +2641,10 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         off += v[k];
     }
     __syncthreads();
+    if (threadIdx.x < NUM_NB && bwork_s[threadIdx.x]) {
+        atomicAdd(&stats->num_work[threadIdx.x], bwork_s[threadIdx.x]);
+        atomicMax(&stats->num_maxw[threadIdx.x], bmax_s[threadIdx.x]);
+    }
     append_block_rows<NUM_NB, PER>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
     if (pub) {
@@ -2648,6 +2690,7 @@ struct NumArgs {
     const int* gna;
     int ubase;               // near union runs of B rows (A*A with verified near groups; 0: off): Bcol /
                              // Bval are then B's arrays extended by the union rows at ubase
+    int wave_bytes;          // grouped wave launches: LDS bytes per wave (0: the template's)
 };
 
 // (forced inline, as num_row: left to the inliner, a grown grouped kernel called them out of
@@ -3154,12 +3197,12 @@ template <int BYTES, bool GROUPED, bool HASH>
 __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int w = threadIdx.x >> 6;
-    char* reg = smem + w * BYTES;
+    char* reg = smem + w * (GROUPED && a.wave_bytes > 0 ? a.wave_bytes : BYTES);  // (grouped: sized to the bin)
     WaveTeam tm;
     auto one = [&](int li) {
         const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
         if constexpr (GROUPED)  // a group head: R rows of one pattern
-            num_row<WaveTeam, false, true, MODES_ALL>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
+            num_row<WaveTeam, false, true, MODES_NOHASH>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
                                                          __builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_RMASK);
         else
             num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH>(tm, a, row, reg + WAVE_HDR,
@@ -3928,20 +3971,34 @@ bool launch_split_bins(const Work& w, const Stats& h, int M, const int* Cptr, hi
     return true;
 }
 
-// Numeric launches of the non-empty bins, largest rows first.  With nss > 1 streams the
-// launches are dealt round-robin over them (launch i on ss[(i + 1) % nss], so the last,
-// bulk wave bins tend to stay on ss[0]): one bin's tail overlaps the next bin's bulk (the
-// reference runs its bins on 12 streams, src/Tool.cu:6-10).  Returns the mask of streams used.
+// Numeric launches of the non-empty bins, dealt over nss streams by estimated duration (LPT:
+// longest first, each onto the least-loaded stream; the reference runs its bins on 12 streams,
+// src/Tool.cu:6-10).  A launch's estimate is the larger of its bulk -- the bin's products (+ a
+// row overhead, k_scan's num_work) over the waves a chip holds -- and its tail -- the heaviest
+// row's products over the waves of one team (a hub row in a 1024-thread block).  The hub rows'
+// launch, long and a few blocks wide, then gets a stream of its own instead of holding a bulk bin
+// queued behind it (wb-edu-like: 3.5 ms idle).  On one stream the launches run longest first.
+// Returns the mask of streams used.
+namespace {
+struct NumLaunch {
+    double cost;
+    int order;                        // (ties: the enumeration order)
+    std::function<void(hipStream_t)> go;
+};
+constexpr double CHIP_WAVES = 4096.0;  // 256 CUs x 16 resident waves
+}  // namespace
+
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
                    double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max, bool split) {
-    int nl = 0, used = 0;
-    auto next_stream = [&]() {
-        const int k = nss > 1 ? (nl + 1) % nss : 0;
-        ++nl;
-        used |= 1 << k;
-        return ss[k];
+    std::vector<NumLaunch> L;
+    auto est = [&](int bin, int team_waves, bool bulk = true, bool tail = true) {
+        const double b = bulk ? (double)h.num_work[bin] / CHIP_WAVES : 0.0;
+        const double t = tail ? (double)h.num_maxw[bin] / team_waves : 0.0;
+        return b > t ? b : t;
     };
-    hipStream_t s = ss[0];
+    auto add = [&](double cost, std::function<void(hipStream_t)> go) {
+        L.push_back(NumLaunch{cost, (int)L.size(), std::move(go)});
+    };
     NumArgs a{};
     a.dense_span_max = dense_span_max;
     a.mcache = w.mcache;
@@ -3978,17 +4035,26 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         a.Bcol = w.bx_col;
         a.Bval = w.bx_val;
     }
+    // a wave-bin launch over `bin`'s list (cursor slot = bin)
+    auto wave_args = [&](int bin) {
+        NumArgs x = a;
+        x.count = h.num_count[bin];
+        x.list = w.bin_list + (long long)(bin - 1) * A.M;
+        x.cursor = w.cursors + bin * 8 * CURSOR_STRIDE;
+        return x;
+    };
 
-    // Numeric-first rows: their copy first (short and HBM-bound: it runs beside the long rows'
-    // launches instead of behind one of them).
+    // Numeric-first rows: their copy of the slot values into C (short and HBM-bound).
     const bool copy = w.sc_col != nullptr;  // numeric-first: tiny classes 0..3 hold slot rows
     if (copy) {
         TinyFused f{};
         int ncopy = 0, cmed = 0;
+        double cost = 0.0;
         for (int c = 3; c >= 0; --c) {
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;
             ncopy += count;
+            cost += est(NUM_TINY + c, 1, true, false);
             const int per = 256 / copy_lanes(c);
             f.c[f.nclass] = c;
             f.count[f.nclass] = count;
@@ -4004,76 +4070,74 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         }
         if (f.nclass > 0) {
             const CopyArgs ca{w.bin_list, A.M, Cptr, w.tslot, w.sc_col, w.sc_val, Ccol, Cval};
-            s = next_stream();
             // lanes per row by the median row's class
-            const int L = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
-            const dim3 grid(round8((A.M + 256 / L - 1) / (256 / L), 16384));
-            if (L == 4) hipLaunchKernelGGL(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
-            else if (L == 8) hipLaunchKernelGGL(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
-            else hipLaunchKernelGGL(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
+            const int Lw = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
+            const dim3 grid(round8((A.M + 256 / Lw - 1) / (256 / Lw), 16384));
+            add(cost * 0.25, [=](hipStream_t s) {  // (a copy: a quarter of a product walk's cost)
+                if (Lw == 4) hipLaunchKernelGGL(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
+                else if (Lw == 8) hipLaunchKernelGGL(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
+                else hipLaunchKernelGGL(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
+            });
         }
     }
-    // Largest bins first so the long rows start early.
     if (h.num_count[NUM_GLOBAL] > 0) {
-        const int count = a.count = h.num_count[NUM_GLOBAL];
-        a.list = w.bin_list + (long long)(NUM_GLOBAL - 1) * A.M;
-        a.cursor = w.cursors + NUM_GLOBAL * 8 * CURSOR_STRIDE;
-        a.gbytes = align16(h.num_global_need);
-        const int g = count < global_grid ? count : global_grid;
-        s = next_stream();
-        hipLaunchKernelGGL((k_num_block<1024, true>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, a);
+        NumArgs x = wave_args(NUM_GLOBAL);
+        x.gbytes = align16(h.num_global_need);
+        const int g = x.count < global_grid ? x.count : global_grid;
+        add(est(NUM_GLOBAL, 16) * 2.0, [=](hipStream_t s) {  // (global-memory tables: slower per product)
+            hipLaunchKernelGGL((k_num_block<1024, true>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
+        });
     }
     // block bins: rows past the bin's LDS split (hub rows) in a launch of their own, so the
     // others run at the occupancy their own tables allow
     auto block_bin = [&](int bin, int k, int T, int grid_cap, int budget, int big_slot) {
         const int count = h.num_count[bin];
         if (count <= 0) return;
-        auto go = [&](const int* list, int rows, int lds, int slot) {
-            a.list = list;
-            a.count = rows;
-            a.cursor = w.cursors + slot * 8 * CURSOR_STRIDE;
-            s = next_stream();
-            if (T == 1024)
-                hipLaunchKernelGGL((k_num_block<1024, false>), dim3(round8(rows, grid_cap)), dim3(1024), lds, s, a);
-            else
-                hipLaunchKernelGGL((k_num_block<256, false>), dim3(round8(rows, grid_cap)), dim3(256), lds, s, a);
+        const int tw = T / 64;
+        auto go = [&](const int* list, int rows, int lds, int slot, double cost) {
+            NumArgs x = a;
+            x.list = list;
+            x.count = rows;
+            x.cursor = w.cursors + slot * 8 * CURSOR_STRIDE;
+            const dim3 grid(round8(rows, grid_cap));
+            add(cost, [=](hipStream_t s) {
+                if (T == 1024) hipLaunchKernelGGL((k_num_block<1024, false>), grid, dim3(1024), lds, s, x);
+                else hipLaunchKernelGGL((k_num_block<256, false>), grid, dim3(256), lds, s, x);
+            });
         };
         if (split && block_split_on(h, k)) {  // k_split_bins: small rows first, hub rows last
             const int big = h.num_block_big[k];
             const int* l = w.split_list + (k ? 0 : (h.num_count[NUM_B1024] > 0 ? h.num_count[NUM_B1024] : 0));
-            go(l + (count - big), big, block_lds(h.num_block_need[k], budget, T), big_slot);
-            go(l, count - big, block_lds(h.num_block_small_need[k], budget, T), bin);
+            go(l + (count - big), big, block_lds(h.num_block_need[k], budget, T), big_slot, est(bin, tw, false, true));
+            go(l, count - big, block_lds(h.num_block_small_need[k], budget, T), bin, est(bin, tw, true, false));
         } else {
-            go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget, T), bin);
+            go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget, T), bin,
+               est(bin, tw));
         }
     };
     block_bin(NUM_B1024, 1, 1024, 256, LDS_MAX - 1024, BLOCK_BIG_SLOT + 1);
     block_bin(NUM_B256, 0, 256, 1024, NUM_B256_BYTES, BLOCK_BIG_SLOT);
     if (h.num_count[NUM_W16H] > 0) {
-        const int count = a.count = h.num_count[NUM_W16H];
-        a.list = w.bin_list + (long long)(NUM_W16H - 1) * A.M;
-        a.cursor = w.cursors + NUM_W16H * 8 * CURSOR_STRIDE;
-        a.qall = count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
-        s = next_stream();
-        hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_W16H_GRID)),
-                           dim3(256), WPB * NUM_W16_BYTES, s, a);
-        a.qall = 0;
+        NumArgs x = wave_args(NUM_W16H);
+        x.qall = x.count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
+        const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_W16H_GRID));
+        add(est(NUM_W16H, 1), [=](hipStream_t s) {
+            hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+        });
     }
     if (h.num_count[NUM_WSH] > 0) {
-        const int count = a.count = h.num_count[NUM_WSH];
-        a.list = w.bin_list + (long long)(NUM_WSH - 1) * A.M;
-        a.cursor = w.cursors + NUM_WSH * 8 * CURSOR_STRIDE;
-        s = next_stream();
-        hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WSX_GRID)),
-                           dim3(256), WPB * NUM_WS_BYTES, s, a);
+        const NumArgs x = wave_args(NUM_WSH);
+        const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WSX_GRID));
+        add(est(NUM_WSH, 1), [=](hipStream_t s) {
+            hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+        });
     }
     if (h.num_count[NUM_W16] > 0) {
-        const int count = a.count = h.num_count[NUM_W16];
-        a.list = w.bin_list + (long long)(NUM_W16 - 1) * A.M;
-        a.cursor = w.cursors + NUM_W16 * 8 * CURSOR_STRIDE;
-        s = next_stream();
-        hipLaunchKernelGGL(k_num_wave_direct<NUM_W16_BYTES>, dim3(round8((count + WPB - 1) / WPB, 2048)), dim3(256),
-                           WPB * NUM_W16_BYTES, s, a);
+        const NumArgs x = wave_args(NUM_W16);
+        const dim3 grid(round8((x.count + WPB - 1) / WPB, 2048));
+        add(est(NUM_W16, 1), [=](hipStream_t s) {
+            hipLaunchKernelGGL(k_num_wave_direct<NUM_W16_BYTES>, grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+        });
     }
     {
         TinyArgs t{};
@@ -4095,15 +4159,17 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             tc.count = count;
             tc.bin = NUM_TINY + c;
             tc.list = w.bin_list + (long long)(tc.bin - 1) * A.M;
-            launch_tiny_num(c, count, tc, next_stream());
+            add(est(NUM_TINY + c, 1, true, false), [=](hipStream_t s) { launch_tiny_num(c, count, tc, s); });
         }
         TinyFused f{};
         static_assert(tiny_w(3) <= 32 && tiny_k(0) <= TINY_FUSED_KMAX && tiny_k(1) <= TINY_FUSED_KMAX &&
                           tiny_k(2) <= TINY_FUSED_KMAX && tiny_k(3) <= TINY_FUSED_KMAX && tiny_w(4) == 64,
                       "classes 0..3 fuse (W <= 32, K <= TINY_FUSED_KMAX)");
+        double cost = 0.0;
         for (int c = 3; c >= 0 && !copy; --c) {  // (numeric-first: copied above)
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;
+            cost += est(NUM_TINY + c, 1, true, false);
             const int per = 256 / tiny_w(c);
             f.c[f.nclass] = c;
             f.count[f.nclass] = count;
@@ -4112,33 +4178,52 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         }
         if (f.nclass > 0) {
             t.list = w.bin_list;
-            s = next_stream();
-            hipLaunchKernelGGL(k_tiny_num_small, dim3(f.blk0[f.nclass]), dim3(256), 256 * TINY_FUSED_KMAX * 8, s, t, f);
+            add(cost, [=](hipStream_t s) {
+                hipLaunchKernelGGL(k_tiny_num_small, dim3(f.blk0[f.nclass]), dim3(256), 256 * TINY_FUSED_KMAX * 8, s, t,
+                                   f);
+            });
         }
     }
+    // grouped bins: LDS regions of their largest group's need, 256-byte steps (k_scan's num_wave_need)
+    auto wave_region = [](int need, int cap) {
+        const int b = (need + 255) & ~255;
+        return need <= 0 || b > cap ? cap : b;
+    };
     if (h.num_count[NUM_W16G] > 0) {
-        const int count = a.count = h.num_count[NUM_W16G];
-        a.list = w.bin_list + (long long)(NUM_W16G - 1) * A.M;
-        a.cursor = w.cursors + NUM_W16G * 8 * CURSOR_STRIDE;
-        s = next_stream();
-        hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true>), dim3(round8((count + WPB - 1) / WPB, 2048)),
-                           dim3(256), WPB * NUM_W16_BYTES, s, a);
+        NumArgs x = wave_args(NUM_W16G);
+        x.wave_bytes = wave_region(h.num_wave_need[1], NUM_W16_BYTES);
+        const dim3 grid(round8((x.count + WPB - 1) / WPB, 2048));
+        add(est(NUM_W16G, 1), [=](hipStream_t s) {
+            hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+        });
     }
     if (h.num_count[NUM_WSG] > 0) {
-        const int count = a.count = h.num_count[NUM_WSG];
-        a.list = w.bin_list + (long long)(NUM_WSG - 1) * A.M;
-        a.cursor = w.cursors + NUM_WSG * 8 * CURSOR_STRIDE;
-        s = next_stream();
-        hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true>), dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WS_GRID)),
-                           dim3(256), WPB * NUM_WSG_BYTES, s, a);
+        NumArgs x = wave_args(NUM_WSG);
+        x.wave_bytes = wave_region(h.num_wave_need[0], NUM_WSG_BYTES);
+        const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WS_GRID));
+        add(est(NUM_WSG, 1), [=](hipStream_t s) {
+            hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+        });
     }
     if (h.num_count[NUM_WS] > 0) {
-        const int count = a.count = h.num_count[NUM_WS];
-        a.list = w.bin_list + (long long)(NUM_WS - 1) * A.M;
-        a.cursor = w.cursors + NUM_WS * 8 * CURSOR_STRIDE;
-        s = next_stream();
-        hipLaunchKernelGGL(k_num_wave_direct<NUM_WS_BYTES>, dim3(round8((count + WPB - 1) / WPB, MHS_NUM_WSX_GRID)),
-                           dim3(256), WPB * NUM_WS_BYTES, s, a);
+        const NumArgs x = wave_args(NUM_WS);
+        const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WSX_GRID));
+        add(est(NUM_WS, 1), [=](hipStream_t s) {
+            hipLaunchKernelGGL(k_num_wave_direct<NUM_WS_BYTES>, grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+        });
+    }
+    // LPT: longest first, each onto the least-loaded stream
+    std::stable_sort(L.begin(), L.end(), [](const NumLaunch& x, const NumLaunch& y) { return x.cost > y.cost; });
+    double load[8] = {};
+    int used = 0;
+    const int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
+    for (const NumLaunch& l : L) {
+        int k = 0;
+        for (int j = 1; j < n; ++j)
+            if (load[j] < load[k]) k = j;
+        load[k] += l.cost;
+        used |= 1 << k;
+        l.go(ss[k]);
     }
     return used;
 }

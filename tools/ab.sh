@@ -4,11 +4,13 @@
 export TMPDIR=/tmp MHS_SYNTH_CACHE=/tmp/mhs_synth
 tag=$1; vs=$2; ms=$3; reps=${4:-7}
 out=gpurun_out/$tag; mkdir -p $out
-# a variant is <dir>[@VAR=value[,VAR=value]]: tools/var/<dir>/libmhspgemm.so run under those env vars
+# a variant is <dir>[@VAR=value[,VAR=value]]: tools/var/<dir>/libmhspgemm.so (or <dir> itself when it
+# holds a '/', e.g. abvar/base or mh-spgemm_amd/mhspgemm for the tree's own) run under those env vars
 for r in 1 2; do for spec in $vs; do
   lib=${spec%%@*}; envs=""; [ "$spec" != "$lib" ] && envs=$(echo ${spec#*@} | tr ',' ' ')
-  v=$(echo $spec | tr '@=,' '___')
-  env $envs timeout -k 10 300 python tools/sweep.py $ms --reps $reps --lib tools/var/$lib > $out/ab_${v}_$r.jsonl 2>$out/ab_${v}_$r.err || { echo "sweep $v failed"; tail -5 $out/ab_${v}_$r.err; exit 1; }
+  libdir=$lib; [[ "$lib" != */* ]] && libdir=tools/var/$lib
+  v=$(echo $spec | tr '@=,/' '____')
+  env $envs timeout -k 10 300 python tools/sweep.py $ms --reps $reps --lib $libdir > $out/ab_${v}_$r.jsonl 2>$out/ab_${v}_$r.err || { echo "sweep $v failed"; tail -5 $out/ab_${v}_$r.err; exit 1; }
   python -c "
 import json,sys
 for l in open('$out/ab_${v}_$r.jsonl'):

@@ -4,7 +4,7 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
-out=$ROOT/tools/var/$name
+out=${OUT:-$ROOT/tools/var}/$name
 mkdir -p $out
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I$ROOT/include "$@" \
     -c $ROOT/mh-spgemm_amd/csrc/mhs_kernels.hip -o $out/mhs_kernels.o
