@@ -80,6 +80,9 @@
 #ifndef MHS_GRP_UNROLL
 #define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
 #endif
+#ifndef MHS_GRP_VEC
+#define MHS_GRP_VEC 1  // full 3-row groups: 3 consecutive entries a lane, one index lookup (run_segment_group_v)
+#endif
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice).  The wave kernels are
 // bound by per-row latency chains, so waves in flight matter more than a few spills.
 #ifndef MHS_WPE_HASH
@@ -1162,9 +1165,11 @@ __device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int 
             for (int i = 0; i < LM; ++i) b[u][i] = f.val(s + o[i] + q);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) {
+            pin(c[u]);  // (every load of the batch issues before the first use: one round trip)
 #pragma unroll
             for (int i = 0; i < LM; ++i) pin(b[u][i]);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (q0 + u * G >= n) break;
@@ -1181,6 +1186,72 @@ __device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int 
                 }
             }
             f.add_rows(c[u], v, R, stride);
+        }
+    }
+}
+
+// Row group over B rows whose columns come in runs of consecutive columns (FEM dof blocks: a
+// node's dofs, and the x-neighbour nodes, are consecutive columns): a lane takes V consecutive
+// entries q .. q+V-1 of the visit (one load batch, one round trip); when their columns are
+// consecutive too, they land in consecutive accumulator slots -- every column of a B row on the
+// walk is in the C row, so the rank of column c+1 is the rank of c plus one -- and one index
+// lookup serves V entries (ds_add_f64's immediate offset covers the rest).  A batch in which
+// any lane's columns are not consecutive (a run edge, a union row) looks every entry up.
+template <int V, int LM, int RM, bool FULL, class F>
+__device__ __forceinline__ void run_segment_group_v(const F& f, int s, int n, int gl, int G,
+                                                    const double (&a)[RM][LM], int L, int R, int stride) {
+    int o[LM];
+#pragma unroll
+    for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
+    for (int q0 = gl * V; q0 < n; q0 += G * V) {
+        int c[V];
+        double b[V][LM];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const int q = q0 + e < n ? q0 + e : n - 1;  // clamped: a cache hit, not accumulated
+            c[e] = f.col(s + q);
+#pragma unroll
+            for (int i = 0; i < LM; ++i) b[e][i] = f.val(s + o[i] + q);
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            pin(c[e]);
+#pragma unroll
+            for (int i = 0; i < LM; ++i) pin(b[e][i]);
+        }
+        const int ne = n - q0 < V ? n - q0 : V;
+        auto sums = [&](int e, double (&v)[RM]) {
+#pragma unroll
+            for (int r = 0; r < RM; ++r) {
+                v[r] = a[r][0] * b[e][0];
+#pragma unroll
+                for (int i = 1; i < LM; ++i) {
+                    if constexpr (FULL) v[r] = fma(a[r][i], b[e][i], v[r]);
+                    else v[r] += i < L ? a[r][i] * b[e][i] : 0.0;
+                }
+            }
+        };
+        // (FEM rows of dof-3 nodes: B rows of 3k entries, every lane holds V whole entries; a
+        // repeated column -- B rows may hold duplicates -- breaks the run)
+        bool cons = ne == V;
+#pragma unroll
+        for (int e = 1; e < V; ++e) cons = cons && c[e] - c[e - 1] == 1;
+        if (__ballot(!cons) == 0) {
+            const int idx = f.index(c[0]);
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                double v[RM];
+                sums(e, v);
+                f.add_rows_idx(idx + e, v, R, stride);
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                if (e >= ne) break;
+                double v[RM];
+                sums(e, v);
+                f.add_rows(c[e], v, R, stride);
+            }
         }
     }
 }
@@ -1285,7 +1356,8 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
     const int lane = lane_id();
     // the chunk's own lane-group width (a row's short last chunk takes wide groups: one
     // load batch for its few visits instead of the row's batches per visit)
-    const int G = chunk_group(x.nh, avg, MHS_GRP_UNROLL, x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
+    const int G = chunk_group(x.nh, avg, RC == 3 && MHS_GRP_VEC ? 3 : MHS_GRP_UNROLL,
+                              x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
     const int gs = 31 - __clz(G);
     const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
     const int iters = (x.nh + ngrp - 1) / ngrp;
@@ -1296,21 +1368,28 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
         const int n0 = __shfl(x.ln, h);
         const int n = e < x.nh ? n0 : 0;
         const int L = __shfl(x.L, h);
+        // full groups of 3 (dof-3 / dof-6 FEM rows: B rows in runs of 9 or 18 consecutive
+        // columns) walk 3 consecutive entries a lane with one index lookup (run_segment_group_v)
+        constexpr int V = RC == 3 && MHS_GRP_VEC ? 3 : 1;
         if (x.lmax == 1) {
             double a[RM][1];
 #pragma unroll
             for (int r = 0; r < RM; ++r) a[r][0] = __shfl(avr[r], h);
-            run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
+            if constexpr (V > 1) run_segment_group_v<V, 1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
+            else run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
         } else {
             double a[RM][3];
 #pragma unroll
             for (int r = 0; r < RM; ++r)
 #pragma unroll
                 for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h + i, 63));
-            if (__ballot(n > 0 && L != 3) == 0)
-                run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
-            else
-                run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
+            if (__ballot(n > 0 && L != 3) == 0) {
+                if constexpr (V > 1) run_segment_group_v<V, 3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
+                else run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
+            } else {
+                if constexpr (V > 1) run_segment_group_v<V, 3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
+                else run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
+            }
         }
     }
 }
@@ -1539,7 +1618,15 @@ struct TileBuild {
 // mode branch).  DENSE: acc[col - colbase].  DIRECT / HASH: product (c, a*b)
 // -> acc[base(tile(c)) + popc(mask & below(c))], the tile found direct-mapped
 // or by probing (always present: it was inserted by the tile build).
-template <bool GM, int MODE>
+// B gathers: O32 -- the value arrays' byte offsets fit 32 bits (nnz(B) + union rows < 2^29, the
+// host's choice): a load is one global_load with an SGPR base and a 32-bit VGPR offset (no 64-bit
+// address arithmetic: two VALU ops and two VGPRs fewer per load in the product walks)
+template <bool O32, class T>
+__device__ __forceinline__ T ld_idx(const T* __restrict__ base, int i) {
+    if constexpr (O32) return *(const T*)((const char*)base + (unsigned)i * (unsigned)sizeof(T));
+    else return base[i];
+}
+template <bool GM, int MODE, bool O32 = false>
 struct Accum {
     static constexpr bool kValues = true;
     static constexpr bool kUnion = true;  // near union runs (see finish_chunk)
@@ -1554,9 +1641,9 @@ struct Accum {
         int c;
         double v;
     };
-    __device__ __forceinline__ Item load(int i) const { return Item{Bcol[i], Bval[i]}; }
-    __device__ __forceinline__ int col(int i) const { return Bcol[i]; }
-    __device__ __forceinline__ double val(int i) const { return Bval[i]; }
+    __device__ __forceinline__ Item load(int i) const { return Item{ld_idx<O32>(Bcol, i), ld_idx<O32>(Bval, i)}; }
+    __device__ __forceinline__ int col(int i) const { return ld_idx<O32>(Bcol, i); }
+    __device__ __forceinline__ double val(int i) const { return ld_idx<O32>(Bval, i); }
     __device__ __forceinline__ void put(const Item& x, double a) const { add(x.c, a * x.v); }
     // acc[column c] += v
     __device__ __forceinline__ void add(int c, double v) const { acc_add<GM>(&acc[index(c)], v); }
@@ -1564,6 +1651,13 @@ struct Accum {
     template <int RM>
     __device__ __forceinline__ void add_rows(int c, const double (&v)[RM], int R, int stride) const {
         const int idx = index(c);
+#pragma unroll
+        for (int r = 0; r < RM; ++r)
+            if (r < R) acc_add<GM>(&acc[idx + r * stride], v[r]);
+    }
+    // row group: slot idx of every accumulator slice r < R += v[r]
+    template <int RM>
+    __device__ __forceinline__ void add_rows_idx(int idx, const double (&v)[RM], int R, int stride) const {
 #pragma unroll
         for (int r = 0; r < RM; ++r)
             if (r < R) acc_add<GM>(&acc[idx + r * stride], v[r]);
@@ -2407,7 +2501,6 @@ __device__ __forceinline__ int num_group_bin_of(int n, int flop, int span, int t
                                                 int nA, bool tiny_ok) {
     if (R < 2 || n == 0 || (tiny_ok && tiny_class(flop, nA, TINY_NUM_SMALL) >= 0))
         return NUM_NONE;  // tiny rows: one by one
-    if (num_mode(span, t, n, dense_span_max) == NM_HASH) return NUM_NONE;  // (grouped kernels: direct tables only)
     const long long need = num_need_rows(span, t, n, dense_span_max, R);
     if (need <= NUM_WSG_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return NUM_WSG;
     if (need <= NUM_W16_BYTES - WAVE_HDR && flop <= NUM_W16_WORK) return NUM_W16G;
@@ -2696,7 +2789,7 @@ struct NumArgs {
 // (forced inline, as num_row: left to the inliner, a grown grouped kernel called them out of
 // line, and the kernel argument they take by reference went to scratch -- 304 bytes a lane,
 // every field read a scratch load)
-template <class Team, bool GLOBALMEM, int MODE, bool GROUPED>
+template <class Team, bool GLOBALMEM, int MODE, bool GROUPED, bool O32>
 __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, int span, int t,
                              int c0, int n, int a0, int a1, char* region, int* counter,
                              int4* stage, int R) {
@@ -2877,7 +2970,7 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
 
     // 3. accumulate every product of the row (of the group's rows)
     {
-        const Accum<GLOBALMEM, MODE> f{E, acc, lo, H, colbase, a.Bcol, a.Bval, a.ubase};
+        const Accum<GLOBALMEM, MODE, O32> f{E, acc, lo, H, colbase, a.Bcol, a.Bval, a.ubase};
         if constexpr (GROUPED) {
             const int nAr = a1 - a0;
             const int avg = nAr > 0 ? (__builtin_amdgcn_readfirstlane(a.rflop[row]) + nAr - 1) / nAr : 1;
@@ -3065,7 +3158,7 @@ __device__ void num_row_wide(const BlockTeam<T, false>& tm, const NumArgs& a, in
 // Numeric rank-by-bitmap row (block kernels): the two tile walks of sym_row_bitmap, the
 // C-row base of every rank by one scan in column order, then each product lands at
 // base[rank] + popc(msk[rank] & below(col)) in an LDS accumulator (no global atomics).
-template <bool GM>
+template <bool GM, bool O32 = false>
 struct RankAccum {
     static constexpr bool kValues = true;
     static constexpr bool kUnion = false;
@@ -3082,9 +3175,9 @@ struct RankAccum {
         int c;
         double v;
     };
-    __device__ __forceinline__ Item load(int i) const { return Item{Bcol[i], Bval[i]}; }
-    __device__ __forceinline__ int col(int i) const { return Bcol[i]; }
-    __device__ __forceinline__ double val(int i) const { return Bval[i]; }
+    __device__ __forceinline__ Item load(int i) const { return Item{ld_idx<O32>(Bcol, i), ld_idx<O32>(Bval, i)}; }
+    __device__ __forceinline__ int col(int i) const { return ld_idx<O32>(Bcol, i); }
+    __device__ __forceinline__ double val(int i) const { return ld_idx<O32>(Bval, i); }
     __device__ __forceinline__ void put(const Item& x, double a) const { add(x.c, a * x.v); }
     __device__ __forceinline__ void add(int c, double v) const {
         const int r = span_rank(bm, wpre, (c >> TILE_SHIFT) - lo);
@@ -3095,7 +3188,7 @@ struct RankAccum {
     __device__ __forceinline__ void add_rows(int, const double (&)[RM], int, int) const {}
 };
 
-template <int T>
+template <int T, bool O32>
 __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, int row, int lo, int span, int t,
                                int c0, int n, int a0, int a1, char* region, int4* stage) {
     const int nw = (span + 63) >> 6;
@@ -3105,10 +3198,12 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
     unsigned long long* msk = (unsigned long long*)(region + sb);
     int2* kb = (int2*)(region + sb + align16((long long)t * 8));
     double* acc = (double*)(region + sb + 2 * align16((long long)t * 8));
+    MHS_STAMP0();
     const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
     const int lofs = (a.mcache && spill_row(span, tflop, t, a.mc_list))
                          ? __builtin_amdgcn_readfirstlane(a.sp.lofs[row])
                          : -1;
+    MHS_STAMP(0);
     for (int i = tm.rank(); i < nw; i += T) bm[i] = 0ull;
     for (int r = tm.rank(); r < t; r += T) msk[r] = 0ull;
     tm.sync();
@@ -3137,13 +3232,17 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
                       RankedMasks{bm, wpre, msk, kb, lo, a.btcol, a.btmask}, stage);
     }
     tm.sync();
+    MHS_STAMP(1);
     tm.exclusive_scan(
         t, [&](int r) { return (int)__popcll(msk[r]); }, [&](int r, int v) { kb[r].y = v; });
+    MHS_STAMP(2);
     for (int r = tm.rank(); r < n; r += T) acc[r] = 0.0;
     tm.sync();
+    MHS_STAMP(3);
     walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, __builtin_amdgcn_readfirstlane(a.rflop[row]),
-                  RankAccum<false>{bm, wpre, msk, kb, acc, lo, a.Bcol, a.Bval}, stage);
+                  RankAccum<false, O32>{bm, wpre, msk, kb, acc, lo, a.Bcol, a.Bval}, stage);
     tm.sync();
+    MHS_STAMP(4);
     for (int r = tm.rank(); r < n; r += T) st_stream(&a.Cval[c0 + r], acc[r]);
     tm.sync();  // the accumulator region now stages the column indices
     int* cb = (int*)acc;
@@ -3159,6 +3258,7 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
     tm.sync();
     for (int r = tm.rank(); r < n; r += T) st_stream(&a.Ccol[c0 + r], cb[r]);
     tm.sync();
+    MHS_STAMP(5);
 }
 
 // MODES: which row bodies a kernel instantiates (the binning sends a row only to a
@@ -3168,7 +3268,7 @@ enum NumModes : int { MODES_ALL = 0, MODES_NOHASH = 1, MODES_HASH = 2 };
 
 // Row-level scalars are made provably wave-uniform (readfirstlane) so that the
 // mode dispatch and every per-row loop bound compile to scalar control flow.
-template <class Team, bool GLOBALMEM, bool GROUPED = false, int MODES = MODES_ALL>
+template <class Team, bool GLOBALMEM, bool GROUPED = false, int MODES = MODES_ALL, bool O32 = false>
 __device__ __forceinline__ void num_row(const Team& tm, const NumArgs& a, int row, char* region, int* counter,
                         int4* stage, int R = 1) {
     const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
@@ -3181,19 +3281,19 @@ __device__ __forceinline__ void num_row(const Team& tm, const NumArgs& a, int ro
     const int a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
     const int mode = num_mode(span, t, n, a.dense_span_max);
     if constexpr (MODES == MODES_HASH) {
-        num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
+        num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED, O32>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
         return;
     }
     if (mode == NM_DENSE)
-        num_row_body<Team, GLOBALMEM, NM_DENSE, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
+        num_row_body<Team, GLOBALMEM, NM_DENSE, GROUPED, O32>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else if (MODES == MODES_NOHASH || mode == NM_DIRECT)
-        num_row_body<Team, GLOBALMEM, NM_DIRECT, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
+        num_row_body<Team, GLOBALMEM, NM_DIRECT, GROUPED, O32>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
     else
-        num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
+        num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED, O32>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
 }
 
 
-template <int BYTES, bool GROUPED, bool HASH>
+template <int BYTES, bool GROUPED, bool HASH, bool O32>
 __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int w = threadIdx.x >> 6;
@@ -3202,10 +3302,10 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     auto one = [&](int li) {
         const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
         if constexpr (GROUPED)  // a group head: R rows of one pattern
-            num_row<WaveTeam, false, true, MODES_NOHASH>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
+            num_row<WaveTeam, false, true, MODES_ALL, O32>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
                                                          __builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_RMASK);
         else
-            num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH>(tm, a, row, reg + WAVE_HDR,
+            num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH, O32>(tm, a, row, reg + WAVE_HDR,
                                                                              (int*)reg, nullptr);
     };
     // The 10 KiB bins (16 KiB before round 3) hold the heaviest wave rows (power-law rows of hundreds of tiles, a
@@ -3239,24 +3339,24 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     }
 }
 
-template <int BYTES, bool GROUPED = false, bool HASH = false>
+template <int BYTES, bool GROUPED = false, bool HASH = false, bool O32 = false>
 #if MHS_WPE_GRP > 0
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_GRP) void k_num_wave(NumArgs a) {
 #else
 __global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
 #endif
-    num_wave_rows<BYTES, GROUPED, HASH>(a);
+    num_wave_rows<BYTES, GROUPED, HASH, O32>(a);
 }
-template <int BYTES>
+template <int BYTES, bool O32 = false>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(BYTES > NUM_WS_BYTES ? MHS_WPE_HASH16 : MHS_WPE_HASH) void k_num_wave_hash(NumArgs a) {
-    num_wave_rows<BYTES, false, true>(a);
+    num_wave_rows<BYTES, false, true, O32>(a);
 }
-template <int BYTES>
+template <int BYTES, bool O32 = false>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_DIRECT) void k_num_wave_direct(NumArgs a) {
-    num_wave_rows<BYTES, false, false>(a);
+    num_wave_rows<BYTES, false, false, O32>(a);
 }
 
-template <int T, bool GLOBALMEM>
+template <int T, bool GLOBALMEM, bool O32 = false>
 __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BlockTeam<T, GLOBALMEM> tm{(long long*)smem};
@@ -3274,7 +3374,7 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
             const int c0 = __builtin_amdgcn_readfirstlane(a.Cptr[row]);
             const int n = __builtin_amdgcn_readfirstlane(a.Cptr[row + 1]) - c0;
             if (num_ranked(hi - lo + 1, t, n, a.dense_span_max)) {
-                num_row_bitmap<T>(tm, a, row, lo, hi - lo + 1, t, c0, n, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
+                num_row_bitmap<T, O32>(tm, a, row, lo, hi - lo + 1, t, c0, n, __builtin_amdgcn_readfirstlane(a.Aptr[row]),
                                   __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]), reg, stage);
                 continue;
             }
@@ -3285,7 +3385,7 @@ __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
                 continue;
             }
         }
-        num_row<BlockTeam<T, GLOBALMEM>, GLOBALMEM>(tm, a, row, reg, counter, stage);
+        num_row<BlockTeam<T, GLOBALMEM>, GLOBALMEM, false, MODES_ALL, O32>(tm, a, row, reg, counter, stage);
     }
 }
 
@@ -3717,21 +3817,18 @@ hipError_t init_kernel_attributes() {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX - 1024);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_sym_rare, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX - 1024);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_num_block<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                LDS_MAX - 1024);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_num_block<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                LDS_MAX - 1024);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_num_wave_direct<NUM_W16_BYTES>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_num_wave_hash<NUM_W16_BYTES>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_num_wave<NUM_W16_BYTES, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    const void* big[] = {(const void*)k_num_block<1024, false, false>, (const void*)k_num_block<1024, false, true>,
+                         (const void*)k_num_block<256, false, false>, (const void*)k_num_block<256, false, true>};
+    for (const void* k : big)
+        if (e == hipSuccess) e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX - 1024);
+    const void* wave[] = {(const void*)k_num_wave_direct<NUM_W16_BYTES, false>,
+                          (const void*)k_num_wave_direct<NUM_W16_BYTES, true>,
+                          (const void*)k_num_wave_hash<NUM_W16_BYTES, false>,
+                          (const void*)k_num_wave_hash<NUM_W16_BYTES, true>,
+                          (const void*)k_num_wave<NUM_W16_BYTES, true, false, false>,
+                          (const void*)k_num_wave<NUM_W16_BYTES, true, false, true>};
+    for (const void* k : wave)
+        if (e == hipSuccess) e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     return e;
 }
 
@@ -4035,6 +4132,9 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         a.Bcol = w.bx_col;
         a.Bval = w.bx_val;
     }
+    // 32-bit byte offsets for the B gathers when B's value array (extended by the union rows)
+    // stays below 4 GiB: nnz(B) + 3 nnz(A) < 2^29 (the reference's int32 CSR allows up to 2^31)
+    const bool o32 = (long long)B.nnz + (w.bx_on ? 3LL * A.nnz : 0) < (1LL << 29);
     // a wave-bin launch over `bin`'s list (cursor slot = bin)
     auto wave_args = [&](int bin) {
         NumArgs x = a;
@@ -4085,7 +4185,8 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         x.gbytes = align16(h.num_global_need);
         const int g = x.count < global_grid ? x.count : global_grid;
         add(est(NUM_GLOBAL, 16) * 2.0, [=](hipStream_t s) {  // (global-memory tables: slower per product)
-            hipLaunchKernelGGL((k_num_block<1024, true>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
+            if (o32) hipLaunchKernelGGL((k_num_block<1024, true, true>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
+            else hipLaunchKernelGGL((k_num_block<1024, true, false>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
         });
     }
     // block bins: rows past the bin's LDS split (hub rows) in a launch of their own, so the
@@ -4101,8 +4202,10 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             x.cursor = w.cursors + slot * 8 * CURSOR_STRIDE;
             const dim3 grid(round8(rows, grid_cap));
             add(cost, [=](hipStream_t s) {
-                if (T == 1024) hipLaunchKernelGGL((k_num_block<1024, false>), grid, dim3(1024), lds, s, x);
-                else hipLaunchKernelGGL((k_num_block<256, false>), grid, dim3(256), lds, s, x);
+                if (T == 1024 && o32) hipLaunchKernelGGL((k_num_block<1024, false, true>), grid, dim3(1024), lds, s, x);
+                else if (T == 1024) hipLaunchKernelGGL((k_num_block<1024, false, false>), grid, dim3(1024), lds, s, x);
+                else if (o32) hipLaunchKernelGGL((k_num_block<256, false, true>), grid, dim3(256), lds, s, x);
+                else hipLaunchKernelGGL((k_num_block<256, false, false>), grid, dim3(256), lds, s, x);
             });
         };
         if (split && block_split_on(h, k)) {  // k_split_bins: small rows first, hub rows last
@@ -4122,21 +4225,24 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         x.qall = x.count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_W16H_GRID));
         add(est(NUM_W16H, 1), [=](hipStream_t s) {
-            hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+            if (o32) hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES, true>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+            else hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
         });
     }
     if (h.num_count[NUM_WSH] > 0) {
         const NumArgs x = wave_args(NUM_WSH);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WSX_GRID));
         add(est(NUM_WSH, 1), [=](hipStream_t s) {
-            hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+            if (o32) hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+            else hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
         });
     }
     if (h.num_count[NUM_W16] > 0) {
         const NumArgs x = wave_args(NUM_W16);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, 2048));
         add(est(NUM_W16, 1), [=](hipStream_t s) {
-            hipLaunchKernelGGL(k_num_wave_direct<NUM_W16_BYTES>, grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+            if (o32) hipLaunchKernelGGL((k_num_wave_direct<NUM_W16_BYTES, true>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+            else hipLaunchKernelGGL((k_num_wave_direct<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
         });
     }
     {
@@ -4194,7 +4300,8 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         x.wave_bytes = wave_region(h.num_wave_need[1], NUM_W16_BYTES);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, 2048));
         add(est(NUM_W16G, 1), [=](hipStream_t s) {
-            hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+            if (o32) hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true, false, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+            else hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true, false, false>), grid, dim3(256), WPB * x.wave_bytes, s, x);
         });
     }
     if (h.num_count[NUM_WSG] > 0) {
@@ -4202,14 +4309,16 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         x.wave_bytes = wave_region(h.num_wave_need[0], NUM_WSG_BYTES);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WS_GRID));
         add(est(NUM_WSG, 1), [=](hipStream_t s) {
-            hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+            if (o32) hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true, false, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+            else hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true, false, false>), grid, dim3(256), WPB * x.wave_bytes, s, x);
         });
     }
     if (h.num_count[NUM_WS] > 0) {
         const NumArgs x = wave_args(NUM_WS);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WSX_GRID));
         add(est(NUM_WS, 1), [=](hipStream_t s) {
-            hipLaunchKernelGGL(k_num_wave_direct<NUM_WS_BYTES>, grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+            if (o32) hipLaunchKernelGGL((k_num_wave_direct<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+            else hipLaunchKernelGGL((k_num_wave_direct<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
         });
     }
     // LPT: longest first, each onto the least-loaded stream

@@ -51,3 +51,11 @@ for a_, b_ in zip(edges[:-1], edges[1:]):
         continue
     print("flop [%d, %d): %d rows, mean total %.0f cycles:" % (a_, b_, sel.sum(), tot_r[sel].mean()),
           " ".join(f"{nm.split('(')[0]}={ph[sel, k].mean():.0f}" for k, nm in enumerate(names)))
+# the ten slowest rows (hub rows: is one row the launch's tail?)
+Cp = None
+order = np.argsort(-tot_r)[:10]
+nA = np.diff(A.ptr)
+print("slowest rows: row, total cycles (ms at 2.4 GHz), flop, nA, phases")
+for r in order:
+    print(f"  {r:9d} {tot_r[r]:12.0f} ({tot_r[r] / 2.4e6:.3f} ms) flop {rf[r]:9d} nA {nA[r]:6d} ",
+          " ".join(f"{ph[r, k]:.0f}" for k in range(6)))
