@@ -80,6 +80,9 @@
 #ifndef MHS_GRP_UNROLL
 #define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
 #endif
+#ifndef MHS_DEAL_RR
+#define MHS_DEAL_RR 0  // 1: numeric launches dealt round-robin (A/B builds only)
+#endif
 #ifndef MHS_GRP_VEC
 #define MHS_GRP_VEC 1  // full 3-row groups: 3 consecutive entries a lane, one index lookup (run_segment_group_v)
 #endif
@@ -1356,7 +1359,7 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
     const int lane = lane_id();
     // the chunk's own lane-group width (a row's short last chunk takes wide groups: one
     // load batch for its few visits instead of the row's batches per visit)
-    const int G = chunk_group(x.nh, avg, RC == 3 && MHS_GRP_VEC ? 3 : MHS_GRP_UNROLL,
+    const int G = chunk_group(x.nh, avg, (RC == 3 || RC == 2) && MHS_GRP_VEC ? RC : MHS_GRP_UNROLL,
                               x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
     const int gs = 31 - __clz(G);
     const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
@@ -1370,7 +1373,8 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
         const int L = __shfl(x.L, h);
         // full groups of 3 (dof-3 / dof-6 FEM rows: B rows in runs of 9 or 18 consecutive
         // columns) walk 3 consecutive entries a lane with one index lookup (run_segment_group_v)
-        constexpr int V = RC == 3 && MHS_GRP_VEC ? 3 : 1;
+        // (groups of 2: dof-2 rows, B rows in runs of 4 or 6 consecutive columns -- pairs)
+        constexpr int V = !MHS_GRP_VEC ? 1 : RC == 3 ? 3 : RC == 2 ? 2 : 1;
         if (x.lmax == 1) {
             double a[RM][1];
 #pragma unroll
@@ -1400,6 +1404,12 @@ __device__ __forceinline__ void group_chunk(const StagedChunk& x, const double (
         group_chunk_r<RG_MAX>(x, avr, avg, f, R, stride);
         return;
     }
+#if MHS_GRP_VEC
+    if (R == 2) {  // dof pairs: 2 consecutive entries a lane
+        group_chunk_r<2>(x, avr, avg, f, R, stride);
+        return;
+    }
+#endif
     group_chunk_r<0>(x, avr, avg, f, R, stride);
 }
 
@@ -4321,11 +4331,19 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             else hipLaunchKernelGGL((k_num_wave_direct<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
         });
     }
+    int used = 0;
+    const int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
+#if MHS_DEAL_RR  // (A/B builds: the round-3 dealing, launch i on stream (i + 1) % n in enumeration order)
+    for (size_t i = 0; i < L.size(); ++i) {
+        const int k = n > 1 ? (int)((i + 1) % n) : 0;
+        used |= 1 << k;
+        L[i].go(ss[k]);
+    }
+    return used;
+#endif
     // LPT: longest first, each onto the least-loaded stream
     std::stable_sort(L.begin(), L.end(), [](const NumLaunch& x, const NumLaunch& y) { return x.cost > y.cost; });
     double load[8] = {};
-    int used = 0;
-    const int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
     for (const NumLaunch& l : L) {
         int k = 0;
         for (int j = 1; j < n; ++j)

@@ -13,6 +13,7 @@
 set -o pipefail
 export TMPDIR=/tmp MHS_SYNTH_CACHE=/tmp/mhs_synth
 tag=$1; mats=$2; modes=${3:-trace}
+libarg=""; [ -n "$PROF_LIB" ] && libarg="--lib $PROF_LIB"  # PROF_LIB=<dir>: profile that library
 out=gpurun_out/$tag; mkdir -p $out
 has() { [[ ",$modes," == *",$1,"* ]]; }
 csv() { find "$1" -name '*kernel_trace.csv' | head -1; }
@@ -23,12 +24,12 @@ fi
 for m in $mats; do
   d=$out/$m; mkdir -p $d
   if has trace; then
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d/trace -o run -- python3 tools/sweep.py $m --reps 5 > $d/sweep.log 2>&1 || { echo "trace $m failed"; tail -5 $d/sweep.log; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d/trace -o run -- python3 tools/sweep.py $m --reps 5 $libarg > $d/sweep.log 2>&1 || { echo "trace $m failed"; tail -5 $d/sweep.log; exit 1; }
     python3 tools/timeline.py "$(csv $d/trace)" > $d/timeline.txt 2>&1
     echo "== $m"; tail -1 $d/sweep.log | cut -c1-300; cat $d/timeline.txt
   fi
   if has serial; then
-    MHS_NUM_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d/serial -o run -- python3 tools/sweep.py $m --reps 5 > $d/serial.log 2>&1 || { echo "serial $m failed"; exit 1; }
+    MHS_NUM_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d/serial -o run -- python3 tools/sweep.py $m --reps 5 $libarg > $d/serial.log 2>&1 || { echo "serial $m failed"; exit 1; }
     python3 tools/timeline.py "$(csv $d/serial)" > $d/timeline_serial.txt 2>&1
     echo "== $m (one stream)"; cat $d/timeline_serial.txt
   fi
@@ -36,7 +37,7 @@ for m in $mats; do
     i=0
     for g in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
       i=$((i+1))
-      MHS_NUM_STREAMS=1 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $g --output-format csv -d $d/pmc_$i -o run -- python3 tools/sweep.py $m --reps 2 > $d/pmc_$i.log 2>&1 || { echo "pmc $g $m failed"; exit 1; }
+      MHS_NUM_STREAMS=1 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $g --output-format csv -d $d/pmc_$i -o run -- python3 tools/sweep.py $m --reps 2 $libarg > $d/pmc_$i.log 2>&1 || { echo "pmc $g $m failed"; exit 1; }
       echo "== $m pmc $g ok"
     done
   fi
