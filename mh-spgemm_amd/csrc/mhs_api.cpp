@@ -345,6 +345,9 @@ int front_pass(mhs_ctx* ctx, const Csr& a, const Csr& b, Work& w, int* Cptr, boo
 int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h);
 
 constexpr int NUM_GLOBAL_GRID = 128;
+#ifndef MHS_MULTI_FLOP_LOG2
+#define MHS_MULTI_FLOP_LOG2 24  // numeric launches over several streams from 2^this products on
+#endif
 
 // The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
 // the aux streams, which join the call's stream again.
@@ -354,7 +357,7 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     // so only when there are at least 3 launches of a product worth it)
     hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
     const int nl = numeric_launches(h);
-    const int nss = (nl >= 3 && h.flop >= (1ull << 24)) ? std::min(ctx->num_streams, nl) : 1;
+    const int nss = (nl >= 3 && h.flop >= (1ull << MHS_MULTI_FLOP_LOG2)) ? std::min(ctx->num_streams, nl) : 1;
     // block bins split by LDS need only where their two launches can run side by side (on
     // one stream the hub rows' launch would no longer overlap the others' bulk)
     const bool split = nss > 1 && ctx->split && launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);

@@ -174,9 +174,6 @@ struct Stats {
     int near_verified;             // ... of which verified (union rows built): B's near union runs
     int nonfinite;                 // k_mask_b met an Inf / NaN in B's values (near groups planned): none
     int num_wave_need[2];                // max LDS bytes of a group in NUM_WSG / NUM_W16G (+ WAVE_HDR)
-    int pad_;
-    unsigned long long num_work[NBINS];  // per numeric bin: products (+ 64 a row) -- launch dealing
-    int num_maxw[NBINS];                 // per numeric bin: the heaviest row's products
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
 // kernel writes it and then `seq`, the host spins on `seq` instead of a stream sync.

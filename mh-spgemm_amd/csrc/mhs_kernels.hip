@@ -80,12 +80,6 @@
 #ifndef MHS_GRP_UNROLL
 #define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
 #endif
-#ifndef MHS_DEAL_RR
-#define MHS_DEAL_RR 0  // 1: numeric launches dealt round-robin (A/B builds only)
-#endif
-#ifndef MHS_GRP_VEC
-#define MHS_GRP_VEC 1  // full 3-row groups: 3 consecutive entries a lane, one index lookup (run_segment_group_v)
-#endif
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice).  The wave kernels are
 // bound by per-row latency chains, so waves in flight matter more than a few spills.
 #ifndef MHS_WPE_HASH
@@ -1193,72 +1187,6 @@ __device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int 
     }
 }
 
-// Row group over B rows whose columns come in runs of consecutive columns (FEM dof blocks: a
-// node's dofs, and the x-neighbour nodes, are consecutive columns): a lane takes V consecutive
-// entries q .. q+V-1 of the visit (one load batch, one round trip); when their columns are
-// consecutive too, they land in consecutive accumulator slots -- every column of a B row on the
-// walk is in the C row, so the rank of column c+1 is the rank of c plus one -- and one index
-// lookup serves V entries (ds_add_f64's immediate offset covers the rest).  A batch in which
-// any lane's columns are not consecutive (a run edge, a union row) looks every entry up.
-template <int V, int LM, int RM, bool FULL, class F>
-__device__ __forceinline__ void run_segment_group_v(const F& f, int s, int n, int gl, int G,
-                                                    const double (&a)[RM][LM], int L, int R, int stride) {
-    int o[LM];
-#pragma unroll
-    for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
-    for (int q0 = gl * V; q0 < n; q0 += G * V) {
-        int c[V];
-        double b[V][LM];
-#pragma unroll
-        for (int e = 0; e < V; ++e) {
-            const int q = q0 + e < n ? q0 + e : n - 1;  // clamped: a cache hit, not accumulated
-            c[e] = f.col(s + q);
-#pragma unroll
-            for (int i = 0; i < LM; ++i) b[e][i] = f.val(s + o[i] + q);
-        }
-#pragma unroll
-        for (int e = 0; e < V; ++e) {
-            pin(c[e]);
-#pragma unroll
-            for (int i = 0; i < LM; ++i) pin(b[e][i]);
-        }
-        const int ne = n - q0 < V ? n - q0 : V;
-        auto sums = [&](int e, double (&v)[RM]) {
-#pragma unroll
-            for (int r = 0; r < RM; ++r) {
-                v[r] = a[r][0] * b[e][0];
-#pragma unroll
-                for (int i = 1; i < LM; ++i) {
-                    if constexpr (FULL) v[r] = fma(a[r][i], b[e][i], v[r]);
-                    else v[r] += i < L ? a[r][i] * b[e][i] : 0.0;
-                }
-            }
-        };
-        // (FEM rows of dof-3 nodes: B rows of 3k entries, every lane holds V whole entries; a
-        // repeated column -- B rows may hold duplicates -- breaks the run)
-        bool cons = ne == V;
-#pragma unroll
-        for (int e = 1; e < V; ++e) cons = cons && c[e] - c[e - 1] == 1;
-        if (__ballot(!cons) == 0) {
-            const int idx = f.index(c[0]);
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-                double v[RM];
-                sums(e, v);
-                f.add_rows_idx(idx + e, v, R, stride);
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-                if (e >= ne) break;
-                double v[RM];
-                sums(e, v);
-                f.add_rows(c[e], v, R, stride);
-            }
-        }
-    }
-}
-
 // One wave's chunks of an A row: [jb0, jb0 + 64), [jb0 + jstep, ...), ... below a1.
 template <class F>
 __device__ __forceinline__ void wave_chunk(const StagedChunk& x, int Grow, const F& f) {
@@ -1359,8 +1287,7 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
     const int lane = lane_id();
     // the chunk's own lane-group width (a row's short last chunk takes wide groups: one
     // load batch for its few visits instead of the row's batches per visit)
-    const int G = chunk_group(x.nh, avg, (RC == 3 || RC == 2) && MHS_GRP_VEC ? RC : MHS_GRP_UNROLL,
-                              x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
+    const int G = chunk_group(x.nh, avg, MHS_GRP_UNROLL, x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
     const int gs = 31 - __clz(G);
     const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
     const int iters = (x.nh + ngrp - 1) / ngrp;
@@ -1371,29 +1298,21 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
         const int n0 = __shfl(x.ln, h);
         const int n = e < x.nh ? n0 : 0;
         const int L = __shfl(x.L, h);
-        // full groups of 3 (dof-3 / dof-6 FEM rows: B rows in runs of 9 or 18 consecutive
-        // columns) walk 3 consecutive entries a lane with one index lookup (run_segment_group_v)
-        // (groups of 2: dof-2 rows, B rows in runs of 4 or 6 consecutive columns -- pairs)
-        constexpr int V = !MHS_GRP_VEC ? 1 : RC == 3 ? 3 : RC == 2 ? 2 : 1;
         if (x.lmax == 1) {
             double a[RM][1];
 #pragma unroll
             for (int r = 0; r < RM; ++r) a[r][0] = __shfl(avr[r], h);
-            if constexpr (V > 1) run_segment_group_v<V, 1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
-            else run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
+            run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
         } else {
             double a[RM][3];
 #pragma unroll
             for (int r = 0; r < RM; ++r)
 #pragma unroll
                 for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h + i, 63));
-            if (__ballot(n > 0 && L != 3) == 0) {
-                if constexpr (V > 1) run_segment_group_v<V, 3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
-                else run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
-            } else {
-                if constexpr (V > 1) run_segment_group_v<V, 3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
-                else run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
-            }
+            if (__ballot(n > 0 && L != 3) == 0)
+                run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
+            else
+                run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
         }
     }
 }
@@ -1404,12 +1323,6 @@ __device__ __forceinline__ void group_chunk(const StagedChunk& x, const double (
         group_chunk_r<RG_MAX>(x, avr, avg, f, R, stride);
         return;
     }
-#if MHS_GRP_VEC
-    if (R == 2) {  // dof pairs: 2 consecutive entries a lane
-        group_chunk_r<2>(x, avr, avg, f, R, stride);
-        return;
-    }
-#endif
     group_chunk_r<0>(x, avr, avg, f, R, stride);
 }
 
@@ -1661,13 +1574,6 @@ struct Accum {
     template <int RM>
     __device__ __forceinline__ void add_rows(int c, const double (&v)[RM], int R, int stride) const {
         const int idx = index(c);
-#pragma unroll
-        for (int r = 0; r < RM; ++r)
-            if (r < R) acc_add<GM>(&acc[idx + r * stride], v[r]);
-    }
-    // row group: slot idx of every accumulator slice r < R += v[r]
-    template <int RM>
-    __device__ __forceinline__ void add_rows_idx(int idx, const double (&v)[RM], int R, int stride) const {
 #pragma unroll
         for (int r = 0; r < RM; ++r)
             if (r < R) acc_add<GM>(&acc[idx + r * stride], v[r]);
@@ -2555,13 +2461,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     __shared__ long long ws[16];
     __shared__ long long excl_s;
     __shared__ int bid_s;
-    __shared__ unsigned long long bwork_s[NUM_NB];  // the block's products (+ a row overhead) per numeric bin
-    __shared__ int bmax_s[NUM_NB];                  // ... and its heaviest row's
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    if (threadIdx.x < NUM_NB) {
-        bwork_s[threadIdx.x] = 0ull;
-        bmax_s[threadIdx.x] = 0;
-    }
     // grids of <= 256 blocks (M <= 256K rows) are co-resident (a 1024-thread block with
     // ~1 KiB of LDS fits any CU), so no block can wait on one that never starts: the
     // block index serves, and the ticket's atomic round trip leaves the critical path
@@ -2642,23 +2542,6 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                   tok);
         }
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
-        {  // work estimate of the row's launch (launch_numeric deals launches by it): products
-           // (a group head: the group's), + 64 for the row's fixed steps
-            const int g0 = i < M ? (int)grp[i] : 0;
-            const int gR = (!(g0 & GRP_CONT) && nbin != NUM_NONE) ? ((g0 & GRP_RMASK) > 1 ? (g0 & GRP_RMASK) : 1) : 1;
-            const long long wr = nbin != NUM_NONE ? (long long)rflop[i] * gR : 0;
-            for (unsigned long long todo = __ballot(nbin != NUM_NONE); todo;) {
-                const int b = __builtin_amdgcn_readfirstlane(__shfl(nbin, __builtin_ctzll(todo)));
-                const unsigned long long mine = __ballot(nbin == b);
-                todo &= ~mine;
-                const unsigned long long sw = wave_sum(nbin == b ? (unsigned long long)wr + 64 : 0ull);
-                const int mw = wave_max(nbin == b ? sat_int(wr) : 0);
-                if (lane == 0) {
-                    atomicAdd(&bwork_s[b], sw);
-                    atomicMax(&bmax_s[b], mw);
-                }
-            }
-        }
         // the grouped wave bins' launches take LDS regions sized to their largest group (a 3-row FEM
         // group needs ~7 KB of the 10 KiB region: 5 waves per SIMD instead of 4)
         {
@@ -2744,10 +2627,6 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         off += v[k];
     }
     __syncthreads();
-    if (threadIdx.x < NUM_NB && bwork_s[threadIdx.x]) {
-        atomicAdd(&stats->num_work[threadIdx.x], bwork_s[threadIdx.x]);
-        atomicMax(&stats->num_maxw[threadIdx.x], bmax_s[threadIdx.x]);
-    }
     append_block_rows<NUM_NB, PER>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
     if (pub) {
@@ -4078,34 +3957,24 @@ bool launch_split_bins(const Work& w, const Stats& h, int M, const int* Cptr, hi
     return true;
 }
 
-// Numeric launches of the non-empty bins, dealt over nss streams by estimated duration (LPT:
-// longest first, each onto the least-loaded stream; the reference runs its bins on 12 streams,
-// src/Tool.cu:6-10).  A launch's estimate is the larger of its bulk -- the bin's products (+ a
-// row overhead, k_scan's num_work) over the waves a chip holds -- and its tail -- the heaviest
-// row's products over the waves of one team (a hub row in a 1024-thread block).  The hub rows'
-// launch, long and a few blocks wide, then gets a stream of its own instead of holding a bulk bin
-// queued behind it (wb-edu-like: 3.5 ms idle).  On one stream the launches run longest first.
+// Numeric launches of the non-empty bins, largest rows first, dealt round-robin over nss streams
+// (launch i on ss[(i + 1) % nss], so the last, bulk wave bins tend to stay on ss[0]): one bin's
+// tail overlaps the next bin's bulk (the reference runs its bins on 12 streams, src/Tool.cu:6-10).
+// Measured (round 4, profiles/r04): dealing by estimated work (LPT over products and the heaviest
+// row) put the hub rows' launch behind the bulk bins -- wb-edu-like +3 %, webbase-like +3 % --
+// concurrent launches share the CUs, and the hub rows' 1024-thread blocks, one per CU for their
+// LDS, progress only as CUs free up; started first, they hold their CUs from the start.
 // Returns the mask of streams used.
 namespace {
 struct NumLaunch {
-    double cost;
-    int order;                        // (ties: the enumeration order)
     std::function<void(hipStream_t)> go;
 };
-constexpr double CHIP_WAVES = 4096.0;  // 256 CUs x 16 resident waves
 }  // namespace
 
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
                    double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max, bool split) {
     std::vector<NumLaunch> L;
-    auto est = [&](int bin, int team_waves, bool bulk = true, bool tail = true) {
-        const double b = bulk ? (double)h.num_work[bin] / CHIP_WAVES : 0.0;
-        const double t = tail ? (double)h.num_maxw[bin] / team_waves : 0.0;
-        return b > t ? b : t;
-    };
-    auto add = [&](double cost, std::function<void(hipStream_t)> go) {
-        L.push_back(NumLaunch{cost, (int)L.size(), std::move(go)});
-    };
+    auto add = [&](std::function<void(hipStream_t)> go) { L.push_back(NumLaunch{std::move(go)}); };
     NumArgs a{};
     a.dense_span_max = dense_span_max;
     a.mcache = w.mcache;
@@ -4159,12 +4028,10 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (copy) {
         TinyFused f{};
         int ncopy = 0, cmed = 0;
-        double cost = 0.0;
         for (int c = 3; c >= 0; --c) {
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;
             ncopy += count;
-            cost += est(NUM_TINY + c, 1, true, false);
             const int per = 256 / copy_lanes(c);
             f.c[f.nclass] = c;
             f.count[f.nclass] = count;
@@ -4183,7 +4050,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             // lanes per row by the median row's class
             const int Lw = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
             const dim3 grid(round8((A.M + 256 / Lw - 1) / (256 / Lw), 16384));
-            add(cost * 0.25, [=](hipStream_t s) {  // (a copy: a quarter of a product walk's cost)
+            add([=](hipStream_t s) {
                 if (Lw == 4) hipLaunchKernelGGL(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
                 else if (Lw == 8) hipLaunchKernelGGL(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
                 else hipLaunchKernelGGL(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
@@ -4194,7 +4061,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         NumArgs x = wave_args(NUM_GLOBAL);
         x.gbytes = align16(h.num_global_need);
         const int g = x.count < global_grid ? x.count : global_grid;
-        add(est(NUM_GLOBAL, 16) * 2.0, [=](hipStream_t s) {  // (global-memory tables: slower per product)
+        add([=](hipStream_t s) {
             if (o32) hipLaunchKernelGGL((k_num_block<1024, true, true>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
             else hipLaunchKernelGGL((k_num_block<1024, true, false>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
         });
@@ -4204,14 +4071,13 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     auto block_bin = [&](int bin, int k, int T, int grid_cap, int budget, int big_slot) {
         const int count = h.num_count[bin];
         if (count <= 0) return;
-        const int tw = T / 64;
-        auto go = [&](const int* list, int rows, int lds, int slot, double cost) {
+        auto go = [&](const int* list, int rows, int lds, int slot) {
             NumArgs x = a;
             x.list = list;
             x.count = rows;
             x.cursor = w.cursors + slot * 8 * CURSOR_STRIDE;
             const dim3 grid(round8(rows, grid_cap));
-            add(cost, [=](hipStream_t s) {
+            add([=](hipStream_t s) {
                 if (T == 1024 && o32) hipLaunchKernelGGL((k_num_block<1024, false, true>), grid, dim3(1024), lds, s, x);
                 else if (T == 1024) hipLaunchKernelGGL((k_num_block<1024, false, false>), grid, dim3(1024), lds, s, x);
                 else if (o32) hipLaunchKernelGGL((k_num_block<256, false, true>), grid, dim3(256), lds, s, x);
@@ -4221,11 +4087,10 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         if (split && block_split_on(h, k)) {  // k_split_bins: small rows first, hub rows last
             const int big = h.num_block_big[k];
             const int* l = w.split_list + (k ? 0 : (h.num_count[NUM_B1024] > 0 ? h.num_count[NUM_B1024] : 0));
-            go(l + (count - big), big, block_lds(h.num_block_need[k], budget, T), big_slot, est(bin, tw, false, true));
-            go(l, count - big, block_lds(h.num_block_small_need[k], budget, T), bin, est(bin, tw, true, false));
+            go(l + (count - big), big, block_lds(h.num_block_need[k], budget, T), big_slot);
+            go(l, count - big, block_lds(h.num_block_small_need[k], budget, T), bin);
         } else {
-            go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget, T), bin,
-               est(bin, tw));
+            go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget, T), bin);
         }
     };
     block_bin(NUM_B1024, 1, 1024, 256, LDS_MAX - 1024, BLOCK_BIG_SLOT + 1);
@@ -4234,7 +4099,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         NumArgs x = wave_args(NUM_W16H);
         x.qall = x.count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_W16H_GRID));
-        add(est(NUM_W16H, 1), [=](hipStream_t s) {
+        add([=](hipStream_t s) {
             if (o32) hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES, true>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
             else hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
         });
@@ -4242,7 +4107,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_WSH] > 0) {
         const NumArgs x = wave_args(NUM_WSH);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WSX_GRID));
-        add(est(NUM_WSH, 1), [=](hipStream_t s) {
+        add([=](hipStream_t s) {
             if (o32) hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
             else hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
         });
@@ -4250,7 +4115,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_W16] > 0) {
         const NumArgs x = wave_args(NUM_W16);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, 2048));
-        add(est(NUM_W16, 1), [=](hipStream_t s) {
+        add([=](hipStream_t s) {
             if (o32) hipLaunchKernelGGL((k_num_wave_direct<NUM_W16_BYTES, true>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
             else hipLaunchKernelGGL((k_num_wave_direct<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
         });
@@ -4275,17 +4140,15 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             tc.count = count;
             tc.bin = NUM_TINY + c;
             tc.list = w.bin_list + (long long)(tc.bin - 1) * A.M;
-            add(est(NUM_TINY + c, 1, true, false), [=](hipStream_t s) { launch_tiny_num(c, count, tc, s); });
+            add([=](hipStream_t s) { launch_tiny_num(c, count, tc, s); });
         }
         TinyFused f{};
         static_assert(tiny_w(3) <= 32 && tiny_k(0) <= TINY_FUSED_KMAX && tiny_k(1) <= TINY_FUSED_KMAX &&
                           tiny_k(2) <= TINY_FUSED_KMAX && tiny_k(3) <= TINY_FUSED_KMAX && tiny_w(4) == 64,
                       "classes 0..3 fuse (W <= 32, K <= TINY_FUSED_KMAX)");
-        double cost = 0.0;
         for (int c = 3; c >= 0 && !copy; --c) {  // (numeric-first: copied above)
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;
-            cost += est(NUM_TINY + c, 1, true, false);
             const int per = 256 / tiny_w(c);
             f.c[f.nclass] = c;
             f.count[f.nclass] = count;
@@ -4294,7 +4157,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         }
         if (f.nclass > 0) {
             t.list = w.bin_list;
-            add(cost, [=](hipStream_t s) {
+            add([=](hipStream_t s) {
                 hipLaunchKernelGGL(k_tiny_num_small, dim3(f.blk0[f.nclass]), dim3(256), 256 * TINY_FUSED_KMAX * 8, s, t,
                                    f);
             });
@@ -4309,7 +4172,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         NumArgs x = wave_args(NUM_W16G);
         x.wave_bytes = wave_region(h.num_wave_need[1], NUM_W16_BYTES);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, 2048));
-        add(est(NUM_W16G, 1), [=](hipStream_t s) {
+        add([=](hipStream_t s) {
             if (o32) hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true, false, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
             else hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true, false, false>), grid, dim3(256), WPB * x.wave_bytes, s, x);
         });
@@ -4318,7 +4181,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         NumArgs x = wave_args(NUM_WSG);
         x.wave_bytes = wave_region(h.num_wave_need[0], NUM_WSG_BYTES);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WS_GRID));
-        add(est(NUM_WSG, 1), [=](hipStream_t s) {
+        add([=](hipStream_t s) {
             if (o32) hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true, false, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
             else hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true, false, false>), grid, dim3(256), WPB * x.wave_bytes, s, x);
         });
@@ -4326,31 +4189,17 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     if (h.num_count[NUM_WS] > 0) {
         const NumArgs x = wave_args(NUM_WS);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WSX_GRID));
-        add(est(NUM_WS, 1), [=](hipStream_t s) {
+        add([=](hipStream_t s) {
             if (o32) hipLaunchKernelGGL((k_num_wave_direct<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
             else hipLaunchKernelGGL((k_num_wave_direct<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
         });
     }
     int used = 0;
     const int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
-#if MHS_DEAL_RR  // (A/B builds: the round-3 dealing, launch i on stream (i + 1) % n in enumeration order)
     for (size_t i = 0; i < L.size(); ++i) {
         const int k = n > 1 ? (int)((i + 1) % n) : 0;
         used |= 1 << k;
         L[i].go(ss[k]);
-    }
-    return used;
-#endif
-    // LPT: longest first, each onto the least-loaded stream
-    std::stable_sort(L.begin(), L.end(), [](const NumLaunch& x, const NumLaunch& y) { return x.cost > y.cost; });
-    double load[8] = {};
-    for (const NumLaunch& l : L) {
-        int k = 0;
-        for (int j = 1; j < n; ++j)
-            if (load[j] < load[k]) k = j;
-        load[k] += l.cost;
-        used |= 1 << k;
-        l.go(ss[k]);
     }
     return used;
 }
