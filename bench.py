@@ -448,7 +448,7 @@ def main():
             out["roofline"]["peak_measured_copy"] = hbm["copy_GBps"]
             out["roofline"]["frac_vs_measured_copy"] = round(achieved / hbm["copy_GBps"], 4)
         out["hbm_peak"] = dict(hbm, spec_GBps=HBM_PEAK_GBPS,
-                               kernels="mhs_hbm_peak: 16 B a lane, 4 in flight, 8 blocks per CU, 2 GiB buffers")
+                               kernels="mhs_hbm_peak: 16 B a lane, 4 in flight, 16 blocks per CU, 2 GiB buffers, cached or nontemporal stores (the better)")
         if configs:
             geo = float(np.exp(np.mean([np.log(c["frac_e2e"]) for c in configs + [
                 {"frac_e2e": b_comp(M_glob, nnzA, nnzC) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}]])))

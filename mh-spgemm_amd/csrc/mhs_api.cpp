@@ -346,7 +346,7 @@ int ensure_gscratch(mhs_ctx* ctx, Work& w, const Stats& h);
 
 constexpr int NUM_GLOBAL_GRID = 128;
 #ifndef MHS_MULTI_FLOP_LOG2
-#define MHS_MULTI_FLOP_LOG2 24  // numeric launches over several streams from 2^this products on
+#define MHS_MULTI_FLOP_LOG2 22  // numeric launches over several streams from 2^this products on (round 4: 24 -> 22, scircuit-like numeric -9 %)
 #endif
 
 // The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
