@@ -712,6 +712,10 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     }
     Work w = make_work(ctx, L, M, A->nnz, B->nnz, B->N, mc_list);
     w.near_b = L.near && same_ab;
+    if (L.near) {
+        w.vcheck = B->val;
+        w.vcheck_n = B->nnz;
+    }
     // device Stats start zeroed: the previous call's k_scan left them so, else a memset
     if (!ctx->stats_zero) MHS_HIP(hipMemsetAsync(w.stats, 0, sizeof(Stats), s));
     ctx->stats_zero = false;  // until this call's k_scan has published and cleared them

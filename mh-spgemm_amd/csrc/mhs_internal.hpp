@@ -172,7 +172,7 @@ struct Stats {
     int an_done;                   // and k_probe_publish blocks finished
     int near_heads;                // near-group candidates listed by k_bin_list (k_near's work)
     int near_verified;             // ... of which verified (union rows built): B's near union runs
-    int nonfinite;                 // k_mask_b met an Inf / NaN in B's values (near groups planned): none
+    int nonfinite;                 // the near check met an Inf / NaN in B's values: k_scan dissolves the near groups
     int num_wave_need[2];                // max LDS bytes of a group in NUM_WSG / NUM_W16G (+ WAVE_HDR)
 };
 // Host-visible copy of Stats (fine-grained pinned memory): the last pre-numeric
@@ -190,7 +190,6 @@ constexpr int ERR_UNSORTED = 1;
 constexpr int ERR_COL_RANGE = 2;
 constexpr int ERR_ACOL_RANGE = 4;
 constexpr int ERR_OVERFLOW = 8;
-constexpr int ERR_NONFINITE = 16;  // (k_mask_b's lane flag only: Stats::nonfinite, never an error)
 
 __host__ __device__ inline int next_pow2(int x) {
     int p = 1;
@@ -376,6 +375,8 @@ struct Work {
     double* bx_val;
     int* ucolx;
     int bx_on;
+    const double* vcheck;    // B's values, checked for Inf / NaN by the near check (near groups planned)
+    long long vcheck_n;
     int tiny_num;            // numeric tiny classes allowed (per row: column span <= TINY_NUM_NMAX + 1)
     // numeric-first tiny rows (big M): the symbolic tiny launch sorts them once, in the
     // numeric classes, and sums their values into slots (sc_*); numeric only copies them

@@ -726,7 +726,7 @@ template <int G>
 __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* __restrict__ ptr,
                                          const int* __restrict__ col, int* __restrict__ btcol,
                                          unsigned long long* __restrict__ btmask, int4* __restrict__ bmeta,
-                                         int* __restrict__ bhi, int& err, const double* __restrict__ vcheck) {
+                                         int* __restrict__ bhi, int& err) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
@@ -760,7 +760,6 @@ __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* 
         const bool head = in && tile != ptile;
         if (in && c < pc) err |= ERR_UNSORTED;
         if (in && (c < 0 || c >= N)) err |= ERR_COL_RANGE;
-        if (vcheck && in && !__builtin_isfinite(vcheck[j])) err |= ERR_NONFINITE;
         // next entry's column: within the chunk from the neighbour lane, at the
         // chunk edge from memory
         const int dn = __shfl_down(c, 1, G);
@@ -811,7 +810,7 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
                                                 const int* __restrict__ col, int* __restrict__ btcol,
                                                 unsigned long long* __restrict__ btmask,
                                                 int4* __restrict__ bmeta, int* __restrict__ bhi,
-                                                Stats* __restrict__ stats, const double* __restrict__ vcheck) {
+                                                Stats* __restrict__ stats) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
@@ -819,20 +818,18 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
     int err = 0;
     bool lng = false;
     if constexpr (G < 64) lng = valid && ptr[row + 1] - ptr[row] > MASK_LONG * G;
-    mask_row<G>(row, valid && !lng, N, ptr, col, btcol, btmask, bmeta, bhi, err, vcheck);
+    mask_row<G>(row, valid && !lng, N, ptr, col, btcol, btmask, bmeta, bhi, err);
     if constexpr (G < 64) {
         for (unsigned long long lb = __ballot(lng && gl == 0); lb; lb &= lb - 1) {
             const int r = __shfl(row, __builtin_ctzll(lb));
-            mask_row<64>(r, true, N, ptr, col, btcol, btmask, bmeta, bhi, err, vcheck);
+            mask_row<64>(r, true, N, ptr, col, btcol, btmask, bmeta, bhi, err);
         }
     }
     if (__any(err != 0)) {
         int werr = err;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) werr |= __shfl_xor(werr, d);
-        // a non-finite B value is not an error: it only turns near row groups off (k_bin_list)
-        if (lane == 0 && (werr & ~ERR_NONFINITE)) atomicOr(&stats->err, werr & ~ERR_NONFINITE);
-        if (lane == 0 && (werr & ERR_NONFINITE)) stats->nonfinite = 1;
+        if (lane == 0) atomicOr(&stats->err, werr);
     }
 }
 
@@ -2073,6 +2070,12 @@ struct NearArgs {
     int* gna;
     int* ucolx;     // union columns for B's near union runs (bx_col + nnzB): at 3 * A0
     int* verified;  // Stats::near_verified
+    // near groups add explicit 0*b (A side) and a*0 (B's union runs) products: B's values (A's
+    // when B is A) are checked for Inf / NaN by the phase's waves, and a non-finite value makes
+    // k_scan dissolve every near group of the call
+    const double* vcheck;
+    long long vcheck_n;
+    int* nonfinite;  // Stats::nonfinite
 };
 #ifndef MHS_NEAR_GRID
 #define MHS_NEAR_GRID 2048  // k_near's block cap
@@ -2088,6 +2091,20 @@ __device__ void near_groups(const NearArgs& p, char* lds, int gw, int nwaves) {
     const int lane = lane_id();
     const WaveTeam tm;
     const int count = __hip_atomic_load(&p.stats->near_heads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (count > 0 && p.vcheck) {  // the finiteness of B's values, a slice a wave (only with candidates)
+        bool bad = false;
+        const long long st = (long long)nwaves * 64;
+        long long i = (long long)gw * 64 + lane;
+        for (; i + 3 * st < p.vcheck_n; i += 4 * st) {  // four loads in flight a lane
+            double x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = p.vcheck[i + u * st];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) bad |= !__builtin_isfinite(x[u]);
+        }
+        for (; i < p.vcheck_n; i += st) bad |= !__builtin_isfinite(p.vcheck[i]);
+        if (__ballot(bad) && lane == 0) *p.nonfinite = 1;
+    }
     bool any = false;  // this wave verified a group (Stats::near_verified: one store a wave, no atomics)
     // every step's loads are independent of each other: three round trips per group
     for (int li = gw; li < count; li += nwaves) {
@@ -2325,9 +2342,6 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
     __shared__ unsigned char lk_s[LK];
     __shared__ int ncand_s, nbase_s;  // the block's near candidates: one counter add per block
     if (threadIdx.x == 0) ncand_s = 0;
-    // a non-finite B value (k_mask_b): no near groups -- their zero-padded products would turn
-    // 0 * Inf into NaN where the reference never forms the product
-    if (nc.list && stats->nonfinite) nc.list = nullptr;
     const long long lbase = (long long)blockIdx.x * (1024 * PER) - RG_BREAK;
     // link of row r to row r-1: 1 = the same A pattern, 2 = a near candidate (see GRP_NEAR;
     // rows of the small-table wave bin only: k_sym_rare checks them after k_sym_common), 0 = none
@@ -2461,10 +2475,15 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     __shared__ long long ws[16];
     __shared__ long long excl_s;
     __shared__ int bid_s;
+    // the block's largest grouped-bin LDS needs [0, 2), block-bin needs [2, 4), their small
+    // launches' needs [4, 6) and hub-row counts [6, 8): LDS first, one global atomic a block
+    __shared__ int agg_s[8];
     const int lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x < 8) agg_s[threadIdx.x] = 0;
     // grids of <= 256 blocks (M <= 256K rows) are co-resident (a 1024-thread block with
     // ~1 KiB of LDS fits any CU), so no block can wait on one that never starts: the
     // block index serves, and the ticket's atomic round trip leaves the critical path
+    const bool nonfin = stats->nonfinite != 0;  // (k_sym_rare's near check, before this launch)
     int bid = blockIdx.x;
     if (gridDim.x > SCAN_TICKET_MIN) {
         if (threadIdx.x == 0) bid_s = atomicAdd(&stats->scan_ticket, 1);
@@ -2512,7 +2531,13 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
             const int n = v[k];
             const int lo = rlo[i], hi = rhi[i];
             const int span = n ? hi - lo + 1 : 0;
-            const int g = grp[i];
+            int g = grp[i];
+            int hrow = (g & GRP_CONT) ? i - (g & 0x7F) : i;
+            int ghd = (g & GRP_CONT) ? grp[hrow] : g;
+            if (nonfin && (ghd & GRP_NEAR)) {  // Inf / NaN in B's values: the near group's rows alone
+                g = ghd = 1;
+                hrow = i;
+            }
             if (bmeta_near) {  // near union runs of B rows (B is A): mark a verified group's head
                 const int R = g & GRP_RMASK;
                 if (!(g & GRP_CONT) && (g & GRP_NEAR) && R >= 2 && R <= MHS_RUN_MAX)
@@ -2521,8 +2546,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
             // a group runs as one item when its R accumulators fit a wave bin; its
             // members decide alike (same C pattern and sizes; flop and A length: the head's)
             // and then stay out
-            const int hrow = (g & GRP_CONT) ? i - (g & 0x7F) : i;
-            const int gh = ((g & GRP_CONT) ? grp[hrow] : g) & GRP_RMASK;
+            const int gh = ghd & GRP_RMASK;
             const int nA = Aptr[i + 1] - Aptr[i];
             const int hflop = gh > 1 ? rflop[hrow] : rflop[i];
             const int hnA = gh > 1 ? Aptr[hrow + 1] - Aptr[hrow] : nA;
@@ -2551,9 +2575,13 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                 gneed = (int)num_need_rows(rhi[i] - rlo[i] + 1, ctiles[i], v[k], dense_span_max, gg > 1 ? gg : 1) +
                         WAVE_HDR;
             }
-            const int gs = wave_max(nbin == NUM_WSG ? gneed : 0), g16 = wave_max(nbin == NUM_W16G ? gneed : 0);
-            if (lane == 0 && gs) atomicMax(&stats->num_wave_need[0], gs);
-            if (lane == 0 && g16) atomicMax(&stats->num_wave_need[1], g16);
+            // (LDS first: one global atomic per wave measured +10 us on cant-like's k_scan --
+            // thousands of waves on one address)
+            if (__ballot(gneed > 0)) {
+                const int gs = wave_max(nbin == NUM_WSG ? gneed : 0), g16 = wave_max(nbin == NUM_W16G ? gneed : 0);
+                if (lane == 0 && gs) atomicMax(&agg_s[0], gs);
+                if (lane == 0 && g16) atomicMax(&agg_s[1], g16);
+            }
         }
         // the block kernels' launches get the LDS their largest row needs (more blocks per
         // CU than a fixed 64 / 157 KiB when the rows are smaller)
@@ -2561,8 +2589,6 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         if (nbin == NUM_B256 || nbin == NUM_B1024)
             need = block_row_need(nbin == NUM_B1024, rlo[i], rhi[i], ctiles[i], v[k], dense_span_max);
         const int n256 = wave_max(nbin == NUM_B256 ? need : 0), n1024 = wave_max(nbin == NUM_B1024 ? need : 0);
-        if (lane == 0 && n256) atomicMax(&stats->num_block_need[0], n256);
-        if (lane == 0 && n1024) atomicMax(&stats->num_block_need[1], n1024);
         if (n256 | n1024) {  // the split launches (B256_SPLIT / B1024_SPLIT)
             const int split = nbin == NUM_B256 ? B256_SPLIT : B1024_SPLIT;
             const bool blk = nbin == NUM_B256 || nbin == NUM_B1024;
@@ -2571,14 +2597,23 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
             const int b256 = __popcll(__ballot(blk && nbin == NUM_B256 && need > split));
             const int b1024 = __popcll(__ballot(blk && nbin == NUM_B1024 && need > split));
             if (lane == 0) {
-                if (s256) atomicMax(&stats->num_block_small_need[0], s256);
-                if (s1024) atomicMax(&stats->num_block_small_need[1], s1024);
-                if (b256) atomicAdd(&stats->num_block_big[0], b256);
-                if (b1024) atomicAdd(&stats->num_block_big[1], b1024);
+                if (n256) atomicMax(&agg_s[2], n256);
+                if (n1024) atomicMax(&agg_s[3], n1024);
+                if (s256) atomicMax(&agg_s[4], s256);
+                if (s1024) atomicMax(&agg_s[5], s1024);
+                if (b256) atomicAdd(&agg_s[6], b256);
+                if (b1024) atomicAdd(&agg_s[7], b1024);
             }
         }
     }
     __syncthreads();
+    if (threadIdx.x < 8 && agg_s[threadIdx.x]) {
+        const int k = threadIdx.x, v = agg_s[k];
+        if (k < 2) atomicMax(&stats->num_wave_need[k], v);
+        else if (k < 4) atomicMax(&stats->num_block_need[k - 2], v);
+        else if (k < 6) atomicMax(&stats->num_block_small_need[k - 4], v);
+        else atomicAdd(&stats->num_block_big[k - 6], v);
+    }
     if (w == 0) {
         // wave 0 looks back over 64 predecessors per round trip: lane l reads block j - l;
         // the nearest inclusive prefix ends the walk, the aggregates above it are summed
@@ -2630,6 +2665,8 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     append_block_rows<NUM_NB, PER>(nbin_of, M, stats->num_count, list, bid);
     if (!last_block_done(&stats->final_done)) return;
     if (pub) {
+        if (nonfin && threadIdx.x == 0) stats->near_verified = 0;  // (no union runs: nothing to copy)
+        __syncthreads();
         publish_stats(stats, pub, seq);
         // the host has its copy: leave the device Stats zeroed for the next call (nothing
         // after this kernel reads them), which saves that call a memset launch
@@ -3609,9 +3646,6 @@ static int round8(long long x, int cap) {
 // would let stale NEAR_HEAD bits reach k_analyze.
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     if (B.M <= 0) return;
-    // near row groups add explicit 0*b / a*0 products: B's values (= A's when B is A) are
-    // checked for Inf / NaN on the way, and a non-finite value turns near groups off
-    const double* vcheck = w.near_list ? B.val : nullptr;
     // about four chunk iterations per row: a wave then holds several rows, whose
     // dependent load chains overlap (measured on gfx950: 64-lane rows were latency-bound)
     const long long avg = B.M > 0 ? B.nnz / B.M : 0;
@@ -3621,12 +3655,12 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     const int rpb = 256 / G;
     const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
     switch (G) {
-    case 2: hipLaunchKernelGGL(k_mask_b<2>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
-    case 4: hipLaunchKernelGGL(k_mask_b<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
-    case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
-    case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
-    case 32: hipLaunchKernelGGL(k_mask_b<32>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
-    default: hipLaunchKernelGGL(k_mask_b<64>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats, vcheck); break;
+    case 2: hipLaunchKernelGGL(k_mask_b<2>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    case 4: hipLaunchKernelGGL(k_mask_b<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    case 32: hipLaunchKernelGGL(k_mask_b<32>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    default: hipLaunchKernelGGL(k_mask_b<64>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
     }
 }
 
@@ -3843,6 +3877,9 @@ static NearArgs near_args(const Csr& A, const Work& w, const int* Cptr) {
     p.gna = w.gna;
     p.ucolx = w.near_b ? w.ucolx : nullptr;  // (B's union runs: B is A)
     p.verified = &w.stats->near_verified;
+    p.vcheck = w.vcheck;
+    p.vcheck_n = w.vcheck_n;
+    p.nonfinite = &w.stats->nonfinite;
     return p;
 }
 

@@ -32,10 +32,10 @@ CLASSES = [
     ("k_near", "symbolic: near row groups"),
     ("k_scan", "numeric binning: row_ptr scan + classification"),
     ("k_split_bins", "numeric binning: block bins split by LDS need"),
-    ("k_num_wave_direct<5120>", "numeric: wave 5 KiB direct"),
-    ("k_num_wave_direct<10240>", "numeric: wave 10 KiB direct"),
-    ("k_num_wave_hash<5120>", "numeric: wave 5 KiB hash"),
-    ("k_num_wave_hash<10240>", "numeric: wave 10 KiB hash"),
+    ("k_num_wave_direct<5120", "numeric: wave 5 KiB direct"),
+    ("k_num_wave_direct<10240", "numeric: wave 10 KiB direct"),
+    ("k_num_wave_hash<5120", "numeric: wave 5 KiB hash"),
+    ("k_num_wave_hash<10240", "numeric: wave 10 KiB hash"),
     ("k_num_wave<10240, true", "numeric: row groups (wave 10 KiB)"),
     ("k_num_block<256", "numeric: 256-thread block"),
     ("k_num_block<1024, false", "numeric: 1024-thread block (hub rows)"),
