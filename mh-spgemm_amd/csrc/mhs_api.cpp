@@ -72,6 +72,7 @@ struct mhs_ctx {
     int num_streams = 4;
     hipStream_t aux[NAUX] = {};
     hipEvent_t fork_ev = nullptr, join_ev[NAUX] = {};
+    hipEvent_t split_ev = nullptr;  // k_split_bins done (the split block launches wait for it)
 };
 
 namespace {
@@ -358,9 +359,6 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
     const int nl = numeric_launches(h);
     const int nss = (nl >= 3 && h.flop >= (1ull << MHS_MULTI_FLOP_LOG2)) ? std::min(ctx->num_streams, nl) : 1;
-    // block bins split by LDS need only where their two launches can run side by side (on
-    // one stream the hub rows' launch would no longer overlap the others' bulk)
-    const bool split = nss > 1 && ctx->split && launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);
     if (nss > 1) {
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         for (int i = 1; i < nss; ++i) {
@@ -368,8 +366,14 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
             MHS_HIP(hipStreamWaitEvent(ss[i], ctx->fork_ev, 0));
         }
     }
-    const int used =
-        launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID, ctx->dense_span_max, split);
+    // block bins split by LDS need only where their two launches can run side by side (on
+    // one stream the hub rows' launch would no longer overlap the others' bulk).  The partition
+    // runs on the call's stream after the fork: only the split launches wait for it (split_ev),
+    // the other bins start at once (wb-edu-like: 0.33 ms off the numeric phase's start)
+    const bool split = nss > 1 && ctx->split && launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);
+    if (split) MHS_HIP(hipEventRecord(ctx->split_ev, s));
+    const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
+                                    ctx->dense_span_max, split, split ? ctx->split_ev : nullptr);
     MHS_HIP(hipGetLastError());
     for (int i = 1; i < nss; ++i)
         if (used & (1 << i)) {
@@ -561,6 +565,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->stream_ev, hipEventDisableTiming);
     if (const char* v = getenv("MHS_NUM_STREAMS")) ctx->num_streams = std::max(1, std::min(atoi(v), mhs_ctx::NAUX + 1));
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->split_ev, hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i + 1 < ctx->num_streams; ++i) {
         e = hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming);
@@ -594,6 +599,7 @@ void mhs_ctx_destroy(mhs_ctx* ctx) {
     mhs_ctx_trim(ctx);  // outstanding C buffers belong to the caller
     if (ctx->stream_ev) (void)hipEventDestroy(ctx->stream_ev);
     if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
+    if (ctx->split_ev) (void)hipEventDestroy(ctx->split_ev);
     for (int i = 0; i < mhs_ctx::NAUX; ++i) {
         if (ctx->aux[i]) {
             (void)hipStreamSynchronize(ctx->aux[i]);

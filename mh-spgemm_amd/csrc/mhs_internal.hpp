@@ -420,7 +420,7 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
                           Published* pub, int seq);
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
                    int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max,
-                   bool split);
+                   bool split, hipEvent_t split_ev = nullptr);
 // numeric launches a call makes for these bin counts (the 32-lane tiny classes share one; a
 // split block bin makes two)
 int numeric_launches(const Stats& h);

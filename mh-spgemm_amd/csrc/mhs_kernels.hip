@@ -1329,32 +1329,48 @@ __device__ __forceinline__ void group_chunk(const StagedChunk& x, const double (
 // are staged in pairs: both chunks' A loads and then both bmeta loads are issued before
 // the first is walked, so the second chunk's two dependent round trips overlap the
 // first chunk's sweeps (a 69-entry FEM row: 63 + 6 entries).
+struct GroupPair {
+    ChunkLoads c0, c1;
+    double avr0[RG_MAX], avr1[RG_MAX];
+};
+// the A-side loads of the pair at jb (chunks of MHS_GRP_CHUNK entries: 63 keeps the 3-entry
+// runs of dof-3 rows whole -- a chunk edge cuts a run: a 1-entry visit in one chunk, a
+// 2-entry one in the next, masked sweeps)
+__device__ __forceinline__ void group_pair_a(GroupPair& p, int jb, int a1, const int* __restrict__ Acol,
+                                             const double* __restrict__ Aval, int R, int nA) {
+    const int lane = lane_id();
+    const int ce0 = min(a1, jb + MHS_GRP_CHUNK), jb1 = ce0, ce1 = min(a1, jb1 + MHS_GRP_CHUNK);
+    p.c0 = load_chunk_a(lane, jb, ce0, Acol, Aval);
+    p.avr0[0] = p.c0.av;
+#pragma unroll
+    for (int r = 1; r < RG_MAX; ++r) p.avr0[r] = (jb + lane < ce0 && r < R) ? Aval[jb + lane + r * nA] : 0.0;
+    p.c1 = load_chunk_a(lane, jb1, ce1, Acol, Aval);
+    p.avr1[0] = p.c1.av;
+#pragma unroll
+    for (int r = 1; r < RG_MAX; ++r) p.avr1[r] = (jb1 + lane < ce1 && r < R) ? Aval[jb1 + lane + r * nA] : 0.0;
+}
+__device__ __forceinline__ void group_pair_meta(GroupPair& p, const int4* __restrict__ bmeta) {
+    load_chunk_meta(p.c0, bmeta);
+    load_chunk_meta(p.c1, bmeta);
+}
+// The walk of a row group whose first pair `p` is loaded (A and bmeta) by the caller -- its
+// round trips overlap the row's tile-table and rank phases (num_row_body).
 template <class F>
-__device__ __forceinline__ void for_products_group(int a0, int a1, const int* __restrict__ Acol,
+__device__ __forceinline__ void for_products_group(GroupPair& p, int a0, int a1, const int* __restrict__ Acol,
                                                    const double* __restrict__ Aval,
                                                    const int4* __restrict__ bmeta, int avg, const F& f,
                                                    int R, int nA, int stride) {
-    constexpr int RM = RG_MAX;
     static_assert(MHS_RUN_MAX <= 3, "grouped walks merge runs of up to 3 B rows");
     const int lane = lane_id();
     const int ub = union_base(f);
-    // chunks of MHS_GRP_CHUNK entries: 63 keeps the 3-entry runs of dof-3 rows whole (a chunk
-    // edge cuts a run: a 1-entry visit in one chunk, a 2-entry one in the next, masked sweeps)
     for (int jb = a0; jb < a1; jb += 2 * MHS_GRP_CHUNK) {
-        const int ce0 = min(a1, jb + MHS_GRP_CHUNK), jb1 = ce0, ce1 = min(a1, jb1 + MHS_GRP_CHUNK);
-        ChunkLoads c0 = load_chunk_a(lane, jb, ce0, Acol, Aval);
-        double avr0[RM], avr1[RM];
-        avr0[0] = c0.av;
-#pragma unroll
-        for (int r = 1; r < RM; ++r) avr0[r] = (jb + lane < ce0 && r < R) ? Aval[jb + lane + r * nA] : 0.0;
-        ChunkLoads c1 = load_chunk_a(lane, jb1, ce1, Acol, Aval);
-        avr1[0] = c1.av;
-#pragma unroll
-        for (int r = 1; r < RM; ++r) avr1[r] = (jb1 + lane < ce1 && r < R) ? Aval[jb1 + lane + r * nA] : 0.0;
-        load_chunk_meta(c0, bmeta);
-        load_chunk_meta(c1, bmeta);
-        group_chunk(finish_chunk(lane, c0, false, ub), avr0, avg, f, R, stride);
-        if (jb1 < a1) group_chunk(finish_chunk(lane, c1, false, ub), avr1, avg, f, R, stride);
+        if (jb != a0) {
+            group_pair_a(p, jb, a1, Acol, Aval, R, nA);
+            group_pair_meta(p, bmeta);
+        }
+        const int jb1 = min(a1, jb + MHS_GRP_CHUNK);
+        group_chunk(finish_chunk(lane, p.c0, false, ub), p.avr0, avg, f, R, stride);
+        if (jb1 < a1) group_chunk(finish_chunk(lane, p.c1, false, ub), p.avr1, avg, f, R, stride);
     }
 }
 
@@ -2730,6 +2746,23 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
     const int stride = GROUPED ? (int)(num_acc_bytes(MODE, span, t, n) / 8) : 0;
     const int nclear = GROUPED ? (R - 1) * stride + nacc : nacc;
 
+    // row groups: the first chunk pair's A loads go out now and its bmeta gathers after the tile
+    // table -- both round trips overlap the table and rank phases instead of opening the walk
+    // (a FEM dof-3 row of 69 entries is one pair: every A-side load of the group)
+    GroupPair gp;
+    bool gnear = false;
+    int gnw = a1 - a0;
+    const int* gcol = a.Acol;
+    const double* gval = a.Aval;
+    if constexpr (GROUPED) {
+        gnear = (__builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_NEAR) != 0;
+        if (gnear) {
+            gnw = __builtin_amdgcn_readfirstlane(a.gna[row]);
+            gcol = a.ucol;
+            gval = a.uval + 2LL * a0;
+        }
+        group_pair_a(gp, a0, a0 + gnw, gcol, gval, R, gnw);
+    }
     // 1. the C row's tile table: the symbolic pass's masks when it kept them,
     //    else rebuilt (same OR pass as symbolic)
     MHS_STAMP(0);
@@ -2794,6 +2827,7 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
     }
     MHS_STAMP(1);
 
+    if constexpr (GROUPED) group_pair_meta(gp, a.bmeta);
     // 2. rank of every tile's first column = prefix popcount in tile order
     if constexpr (MODE != NM_HASH) {
         tm.exclusive_scan(
@@ -2902,11 +2936,9 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
             const int avg = nAr > 0 ? (__builtin_amdgcn_readfirstlane(a.rflop[row]) + nAr - 1) / nAr : 1;
             // a near group walks its union row (columns at the head's A offset, R value slices
             // nU apart from 3 * Aptr[head]): row r's value of union entry j at uv[a0 + j + r * nU]
-            // with uv = uval + 2 * a0.  (One call site: two inlined walks doubled the registers.)
-            const bool nearg = (__builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_NEAR) != 0;
-            const int nw = nearg ? __builtin_amdgcn_readfirstlane(a.gna[row]) : nAr;
-            for_products_group(a0, a0 + nw, nearg ? a.ucol : a.Acol, nearg ? a.uval + 2LL * a0 : a.Aval, a.bmeta, avg,
-                               f, R, nw, stride);
+            // with uv = uval + 2 * a0 (gcol / gval above).  (One call site: two inlined walks
+            // doubled the registers.)
+            for_products_group(gp, a0, a0 + gnw, gcol, gval, a.bmeta, avg, f, R, gnw, stride);
         } else {
             walk_products(tm, a0, a1, a.Acol, a.Aval, a.bmeta, false, a.rflop[row], f, stage);
         }
@@ -4009,7 +4041,8 @@ struct NumLaunch {
 }  // namespace
 
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
-                   double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max, bool split) {
+                   double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max, bool split,
+                   hipEvent_t split_ev) {
     std::vector<NumLaunch> L;
     auto add = [&](std::function<void(hipStream_t)> go) { L.push_back(NumLaunch{std::move(go)}); };
     NumArgs a{};
@@ -4108,13 +4141,15 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     auto block_bin = [&](int bin, int k, int T, int grid_cap, int budget, int big_slot) {
         const int count = h.num_count[bin];
         if (count <= 0) return;
-        auto go = [&](const int* list, int rows, int lds, int slot) {
+        auto go = [&](const int* list, int rows, int lds, int slot, hipEvent_t after) {
             NumArgs x = a;
             x.list = list;
             x.count = rows;
             x.cursor = w.cursors + slot * 8 * CURSOR_STRIDE;
             const dim3 grid(round8(rows, grid_cap));
+            const hipStream_t s0 = ss[0];
             add([=](hipStream_t s) {
+                if (after && s != s0) (void)hipStreamWaitEvent(s, after, 0);  // (k_split_bins' lists)
                 if (T == 1024 && o32) hipLaunchKernelGGL((k_num_block<1024, false, true>), grid, dim3(1024), lds, s, x);
                 else if (T == 1024) hipLaunchKernelGGL((k_num_block<1024, false, false>), grid, dim3(1024), lds, s, x);
                 else if (o32) hipLaunchKernelGGL((k_num_block<256, false, true>), grid, dim3(256), lds, s, x);
@@ -4124,10 +4159,10 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         if (split && block_split_on(h, k)) {  // k_split_bins: small rows first, hub rows last
             const int big = h.num_block_big[k];
             const int* l = w.split_list + (k ? 0 : (h.num_count[NUM_B1024] > 0 ? h.num_count[NUM_B1024] : 0));
-            go(l + (count - big), big, block_lds(h.num_block_need[k], budget, T), big_slot);
-            go(l, count - big, block_lds(h.num_block_small_need[k], budget, T), bin);
+            go(l + (count - big), big, block_lds(h.num_block_need[k], budget, T), big_slot, split_ev);
+            go(l, count - big, block_lds(h.num_block_small_need[k], budget, T), bin, split_ev);
         } else {
-            go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget, T), bin);
+            go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget, T), bin, nullptr);
         }
     };
     block_bin(NUM_B1024, 1, 1024, 256, LDS_MAX - 1024, BLOCK_BIG_SLOT + 1);

@@ -79,12 +79,13 @@ def stats(d: Path):
 def main():
     tag, head = sys.argv[1], sys.argv[2]
     src = ROOT / "gpurun_out" / tag
-    mats = sys.argv[3:] or sorted(p.name for p in src.iterdir() if (p / "pmc_1").exists())
+    mats = [m for m in sys.argv[3:] if m != "--fresh"] or sorted(p.name for p in src.iterdir() if (p / "pmc_1").exists())
     sf = ROOT / "profiles" / "pmc_summary.json"
-    summary = {"head": head, "note": "per matrix: every kernel of one tools/sweep.py call on this head "
-               "(numeric bins on one stream for attribution); hbm_bytes_per_call = (2*FETCH_SIZE + WRITE_SIZE) "
-               "* 1024 per launch x launches per call (gfx950 correction), separate --pmc passes; "
-               "tcc_hit = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)", "matrices": {}}
+    # merged into the committed summary (--fresh: start over); every matrix names its head
+    summary = {"matrices": {}}
+    if sf.exists() and "--fresh" not in sys.argv:
+        summary = json.loads(sf.read_text())
+    mats = [m for m in mats if m != "--fresh"]
     for m in mats:
         d = src / m
         dst = ROOT / "profiles" / tag / m
@@ -117,11 +118,17 @@ def main():
                 "tcc_hit": round(h / (h + ms), 3) if h + ms > 0 else None,
             }
         (dst / "pmc_per_kernel.json").write_text(json.dumps(per, indent=1) + "\n")
-        summary["matrices"][m] = {"source": f"profiles/{tag}/{m}/pmc_per_kernel.json", "kernels": per}
+        summary["matrices"][m] = {"source": f"profiles/{tag}/{m}/pmc_per_kernel.json", "head": head, "kernels": per}
         print(f"== {m}")
         for k, v in per.items():
             print(f"  {k[:40]:40s} {v['bin_class'][:36]:36s} us {v['avg_us'] or 0:9.1f} "
                   f"GB/s {v['hbm_GBps'] or 0:8.1f} hit {v['tcc_hit']}")
+    heads = sorted({v.get("head", "?") for v in summary["matrices"].values()})
+    summary["head"] = heads[0] if len(heads) == 1 else ",".join(heads)
+    summary["note"] = ("per matrix: every kernel of one tools/sweep.py call on the matrix's head (numeric bins "
+                       "on one stream for attribution); hbm_bytes_per_call = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
+                       "per launch x launches per call (gfx950 correction), separate --pmc passes; "
+                       "tcc_hit = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)")
     sf.write_text(json.dumps(summary, indent=1) + "\n")
 
 
