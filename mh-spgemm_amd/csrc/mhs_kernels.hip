@@ -80,6 +80,12 @@
 #ifndef MHS_GRP_UNROLL
 #define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
 #endif
+#ifndef MHS_OUT_VEC
+#define MHS_OUT_VEC 0  // wave rows write C with 16-byte stores (C.col staged in LDS)
+#endif
+#ifndef MHS_GRP_PAIRS
+#define MHS_GRP_PAIRS 0  // row-group walk: two consecutive entries a lane in one load (run_segment_group_pairs)
+#endif
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice).  The wave kernels are
 // bound by per-row latency chains, so waves in flight matter more than a few spills.
 #ifndef MHS_WPE_HASH
@@ -233,6 +239,12 @@ __device__ __forceinline__ T ld_cache(const T* p) {
     return *p;
 }
 
+// Two consecutive entries in one load (8-byte aligned doubles, 4-byte aligned ints: gfx950 loads
+// them unaligned as one global_load_dwordx4 / _dwordx2)
+typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
+typedef int i2u __attribute__((ext_vector_type(2), aligned(4)));
+typedef int i4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef int i4a __attribute__((ext_vector_type(4), aligned(16)));
 // Lane-group width for walking the products of one row: groups of G lanes
 // take one A entry each and stride its B row.  Pick G minimising the sweeps
 // ceil(nA / groups) * ceil(avg B-row length / G) (ties -> wider, better
@@ -1184,6 +1196,73 @@ __device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int 
     }
 }
 
+// The row-group walk with two consecutive entries a lane in one load each (MHS_GRP_PAIRS): a
+// pair's columns in one global_load_dwordx2, each run row's two values in one _dwordx4 -- half
+// the vector-memory instructions of the entry-a-lane walk (the grouped kernel's loads, 8 bytes a
+// lane, are issue-bound in the texture pipeline: stamps put 2/3 of a cant-like group's cycles in
+// its walk at ~50 % VALU issue).  Segments of one entry take single loads.
+template <int LM, int RM, bool FULL, class F>
+__device__ __forceinline__ void run_segment_group_pairs(const F& f, int s, int n, int gl, int G,
+                                                        const double (&a)[RM][LM], int L, int R, int stride) {
+    constexpr int UP = MHS_GRP_PAIRS > 0 ? MHS_GRP_PAIRS : 1;  // pairs a lane issues together
+    int o[LM];
+#pragma unroll
+    for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
+    for (int q0 = 2 * gl; q0 < n; q0 += UP * 2 * G) {
+        int c[UP][2];
+        double b[UP][LM][2];
+        bool vx[UP], vy[UP];
+#pragma unroll
+        for (int p = 0; p < UP; ++p) {
+            const int q = q0 + p * 2 * G;
+            vx[p] = q + 1 < n;  // entry q (the pair's first)
+            vy[p] = q < n;      // entry q + 1, or n - 1 for the segment's odd tail
+            // a pair inside the segment: (q, q+1), the tail's (n-2, n-1), beyond it any (a cache hit)
+            const int qp = q + 1 < n ? q : (n >= 2 ? n - 2 : 0);
+            if (n >= 2) {
+                const i2u cc = f.col2(s + qp);
+                c[p][0] = cc.x;
+                c[p][1] = cc.y;
+#pragma unroll
+                for (int i = 0; i < LM; ++i) {
+                    const d2u vv = f.val2(s + o[i] + qp);
+                    b[p][i][0] = vv.x;
+                    b[p][i][1] = vv.y;
+                }
+            } else {  // one entry (its neighbour may lie past B's arrays)
+                c[p][0] = c[p][1] = f.col(s);
+#pragma unroll
+                for (int i = 0; i < LM; ++i) b[p][i][0] = b[p][i][1] = f.val(s + o[i]);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < UP; ++p)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                pin(c[p][e]);
+#pragma unroll
+                for (int i = 0; i < LM; ++i) pin(b[p][i][e]);
+            }
+#pragma unroll
+        for (int p = 0; p < UP; ++p)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                if (!(e == 0 ? vx[p] : vy[p])) continue;
+                double v[RM];
+#pragma unroll
+                for (int r = 0; r < RM; ++r) {
+                    v[r] = a[r][0] * b[p][0][e];
+#pragma unroll
+                    for (int i = 1; i < LM; ++i) {
+                        if constexpr (FULL) v[r] = fma(a[r][i], b[p][i][e], v[r]);
+                        else v[r] += i < L ? a[r][i] * b[p][i][e] : 0.0;
+                    }
+                }
+                f.add_rows(c[p][e], v, R, stride);
+            }
+    }
+}
+
 // One wave's chunks of an A row: [jb0, jb0 + 64), [jb0 + jstep, ...), ... below a1.
 template <class F>
 __device__ __forceinline__ void wave_chunk(const StagedChunk& x, int Grow, const F& f) {
@@ -1284,7 +1363,7 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
     const int lane = lane_id();
     // the chunk's own lane-group width (a row's short last chunk takes wide groups: one
     // load batch for its few visits instead of the row's batches per visit)
-    const int G = chunk_group(x.nh, avg, MHS_GRP_UNROLL, x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
+    const int G = chunk_group(x.nh, avg, MHS_GRP_PAIRS ? 2 * MHS_GRP_PAIRS : MHS_GRP_UNROLL, x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
     const int gs = 31 - __clz(G);
     const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
     const int iters = (x.nh + ngrp - 1) / ngrp;
@@ -1299,17 +1378,21 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
             double a[RM][1];
 #pragma unroll
             for (int r = 0; r < RM; ++r) a[r][0] = __shfl(avr[r], h);
-            run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
+            if constexpr (MHS_GRP_PAIRS) run_segment_group_pairs<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
+            else run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
         } else {
             double a[RM][3];
 #pragma unroll
             for (int r = 0; r < RM; ++r)
 #pragma unroll
                 for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h + i, 63));
-            if (__ballot(n > 0 && L != 3) == 0)
-                run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
-            else
-                run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
+            if (__ballot(n > 0 && L != 3) == 0) {
+                if constexpr (MHS_GRP_PAIRS) run_segment_group_pairs<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
+                else run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
+            } else {
+                if constexpr (MHS_GRP_PAIRS) run_segment_group_pairs<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
+                else run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
+            }
         }
     }
 }
@@ -1562,6 +1645,11 @@ __device__ __forceinline__ T ld_idx(const T* __restrict__ base, int i) {
     if constexpr (O32) return *(const T*)((const char*)base + (unsigned)i * (unsigned)sizeof(T));
     else return base[i];
 }
+template <bool O32, class V, class T>
+__device__ __forceinline__ V ld_pair(const T* __restrict__ base, int i) {
+    if constexpr (O32) return *(const V*)((const char*)base + (unsigned)i * (unsigned)sizeof(T));
+    else return *(const V*)(base + i);
+}
 template <bool GM, int MODE, bool O32 = false>
 struct Accum {
     static constexpr bool kValues = true;
@@ -1580,6 +1668,8 @@ struct Accum {
     __device__ __forceinline__ Item load(int i) const { return Item{ld_idx<O32>(Bcol, i), ld_idx<O32>(Bval, i)}; }
     __device__ __forceinline__ int col(int i) const { return ld_idx<O32>(Bcol, i); }
     __device__ __forceinline__ double val(int i) const { return ld_idx<O32>(Bval, i); }
+    __device__ __forceinline__ i2u col2(int i) const { return ld_pair<O32, i2u>(Bcol, i); }
+    __device__ __forceinline__ d2u val2(int i) const { return ld_pair<O32, d2u>(Bval, i); }
     __device__ __forceinline__ void put(const Item& x, double a) const { add(x.c, a * x.v); }
     // acc[column c] += v
     __device__ __forceinline__ void add(int c, double v) const { acc_add<GM>(&acc[index(c)], v); }
@@ -2959,6 +3049,60 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
                     st_part(&a.Ccol[pos + g * n], colbase + (s << TILE_SHIFT) + lane);
                     st_part(&a.Cval[pos + g * n], acc[g * stride + (s << TILE_SHIFT) + lane]);
                 }
+            }
+        }
+    } else if (MHS_OUT_VEC && Team::size == 64) {
+        // wave rows: C.val two a lane and C.col four a lane (16-byte stores: half and a quarter of
+        // the store instructions; the accumulator slices are 16-byte aligned), the columns staged
+        // in LDS by tile (a lane per tile of <= 8 columns, else the wave, lane = bit)
+        const int lane = lane_id();
+        for (int g = 0; g < (GROUPED ? R : 1); ++g) {
+            double* dst = a.Cval + c0 + g * n;
+            const double* src = acc + g * stride;
+            for (int r = 2 * lane; r < n; r += 128) {
+                if (r + 1 < n) __builtin_nontemporal_store(*(const d2u*)(src + r), (d2u*)(dst + r));
+                else st_stream(dst + r, src[r]);
+            }
+        }
+        wave_sync();
+        int* cb = (int*)acc;
+        for (int s0 = 0; s0 < H; s0 += 64) {
+            const int s = s0 + lane;
+            unsigned long long mk = 0;
+            int key = 0, base = 0;
+            if (s < H) {
+                const TileEntry e = E[s];
+                mk = e.mask;
+                key = MODE != NM_HASH ? lo + s : e.key;
+                base = e.base;
+            }
+            const bool big = __popcll(mk) > 8;
+            unsigned long long bigs = __ballot(big);
+            if (!big) {
+                int r = base;
+                while (mk) {
+                    cb[r++] = (key << TILE_SHIFT) + __builtin_ctzll(mk);
+                    mk &= mk - 1;
+                }
+            }
+            while (bigs) {  // the tile's entry re-read by every lane (a broadcast LDS read)
+                const int src = __builtin_ctzll(bigs);
+                bigs &= bigs - 1;
+                const uint4 q = *reinterpret_cast<const uint4*>(&E[s0 + src]);  // mask, base, key
+                const unsigned long long m2 = ((unsigned long long)q.y << 32) | q.x;
+                const int k2 = MODE != NM_HASH ? lo + s0 + src : (int)q.w;
+                if ((m2 >> lane) & 1ull) cb[(int)q.z + __popcll(m2 & lanemask_lt())] = (k2 << TILE_SHIFT) + lane;
+            }
+        }
+        wave_sync();
+        for (int r = 4 * lane; r < n; r += 256) {
+            if (r + 3 < n) {
+                const i4a c4 = *(const i4a*)(cb + r);
+                for (int g = 0; g < (GROUPED ? R : 1); ++g)
+                    __builtin_nontemporal_store((i4u)c4, (i4u*)(a.Ccol + c0 + g * n + r));
+            } else {
+                for (int k = r; k < n; ++k)
+                    for (int g = 0; g < (GROUPED ? R : 1); ++g) st_stream(&a.Ccol[c0 + g * n + k], cb[k]);
             }
         }
     } else {
