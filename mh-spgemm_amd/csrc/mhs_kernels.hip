@@ -80,12 +80,6 @@
 #ifndef MHS_GRP_UNROLL
 #define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
 #endif
-#ifndef MHS_OUT_VEC
-#define MHS_OUT_VEC 0  // wave rows write C with 16-byte stores (C.col staged in LDS)
-#endif
-#ifndef MHS_GRP_PAIRS
-#define MHS_GRP_PAIRS 0  // row-group walk: two consecutive entries a lane in one load (run_segment_group_pairs)
-#endif
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice).  The wave kernels are
 // bound by per-row latency chains, so waves in flight matter more than a few spills.
 #ifndef MHS_WPE_HASH
@@ -95,7 +89,7 @@
 #define MHS_SYM_B256_GRID 1024  // block cap of the persistent 256-thread symbolic bin launch
 #endif
 #ifndef MHS_WPE_HASH16
-#define MHS_WPE_HASH16 MHS_WPE_HASH  // the 10 KiB hash bin (LDS: 4 blocks = 4 waves per SIMD)
+#define MHS_WPE_HASH16 4  // the 10 KiB hash bin: LDS allows 4 waves per SIMD (an 8-wave register target spilled 34 VGPRs for nothing)
 #endif
 #ifndef MHS_WPE_GRP
 #define MHS_WPE_GRP 0  // occupancy floor of the generic / grouped wave numeric kernel (0: compiler's choice)
@@ -1196,73 +1190,6 @@ __device__ __forceinline__ void run_segment_group(const F& f, int s, int n, int 
     }
 }
 
-// The row-group walk with two consecutive entries a lane in one load each (MHS_GRP_PAIRS): a
-// pair's columns in one global_load_dwordx2, each run row's two values in one _dwordx4 -- half
-// the vector-memory instructions of the entry-a-lane walk (the grouped kernel's loads, 8 bytes a
-// lane, are issue-bound in the texture pipeline: stamps put 2/3 of a cant-like group's cycles in
-// its walk at ~50 % VALU issue).  Segments of one entry take single loads.
-template <int LM, int RM, bool FULL, class F>
-__device__ __forceinline__ void run_segment_group_pairs(const F& f, int s, int n, int gl, int G,
-                                                        const double (&a)[RM][LM], int L, int R, int stride) {
-    constexpr int UP = MHS_GRP_PAIRS > 0 ? MHS_GRP_PAIRS : 1;  // pairs a lane issues together
-    int o[LM];
-#pragma unroll
-    for (int i = 0; i < LM; ++i) o[i] = i < L ? i * n : 0;
-    for (int q0 = 2 * gl; q0 < n; q0 += UP * 2 * G) {
-        int c[UP][2];
-        double b[UP][LM][2];
-        bool vx[UP], vy[UP];
-#pragma unroll
-        for (int p = 0; p < UP; ++p) {
-            const int q = q0 + p * 2 * G;
-            vx[p] = q + 1 < n;  // entry q (the pair's first)
-            vy[p] = q < n;      // entry q + 1, or n - 1 for the segment's odd tail
-            // a pair inside the segment: (q, q+1), the tail's (n-2, n-1), beyond it any (a cache hit)
-            const int qp = q + 1 < n ? q : (n >= 2 ? n - 2 : 0);
-            if (n >= 2) {
-                const i2u cc = f.col2(s + qp);
-                c[p][0] = cc.x;
-                c[p][1] = cc.y;
-#pragma unroll
-                for (int i = 0; i < LM; ++i) {
-                    const d2u vv = f.val2(s + o[i] + qp);
-                    b[p][i][0] = vv.x;
-                    b[p][i][1] = vv.y;
-                }
-            } else {  // one entry (its neighbour may lie past B's arrays)
-                c[p][0] = c[p][1] = f.col(s);
-#pragma unroll
-                for (int i = 0; i < LM; ++i) b[p][i][0] = b[p][i][1] = f.val(s + o[i]);
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < UP; ++p)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                pin(c[p][e]);
-#pragma unroll
-                for (int i = 0; i < LM; ++i) pin(b[p][i][e]);
-            }
-#pragma unroll
-        for (int p = 0; p < UP; ++p)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                if (!(e == 0 ? vx[p] : vy[p])) continue;
-                double v[RM];
-#pragma unroll
-                for (int r = 0; r < RM; ++r) {
-                    v[r] = a[r][0] * b[p][0][e];
-#pragma unroll
-                    for (int i = 1; i < LM; ++i) {
-                        if constexpr (FULL) v[r] = fma(a[r][i], b[p][i][e], v[r]);
-                        else v[r] += i < L ? a[r][i] * b[p][i][e] : 0.0;
-                    }
-                }
-                f.add_rows(c[p][e], v, R, stride);
-            }
-    }
-}
-
 // One wave's chunks of an A row: [jb0, jb0 + 64), [jb0 + jstep, ...), ... below a1.
 template <class F>
 __device__ __forceinline__ void wave_chunk(const StagedChunk& x, int Grow, const F& f) {
@@ -1363,7 +1290,7 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
     const int lane = lane_id();
     // the chunk's own lane-group width (a row's short last chunk takes wide groups: one
     // load batch for its few visits instead of the row's batches per visit)
-    const int G = chunk_group(x.nh, avg, MHS_GRP_PAIRS ? 2 * MHS_GRP_PAIRS : MHS_GRP_UNROLL, x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
+    const int G = chunk_group(x.nh, avg, MHS_GRP_UNROLL, x.lmax > 1 ? MHS_RUN_GMIN : MHS_VAL_GMIN);
     const int gs = 31 - __clz(G);
     const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
     const int iters = (x.nh + ngrp - 1) / ngrp;
@@ -1378,21 +1305,17 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
             double a[RM][1];
 #pragma unroll
             for (int r = 0; r < RM; ++r) a[r][0] = __shfl(avr[r], h);
-            if constexpr (MHS_GRP_PAIRS) run_segment_group_pairs<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
-            else run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
+            run_segment_group<1, RM, true>(f, sb, n, gl, G, a, 1, R, stride);
         } else {
             double a[RM][3];
 #pragma unroll
             for (int r = 0; r < RM; ++r)
 #pragma unroll
                 for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h + i, 63));
-            if (__ballot(n > 0 && L != 3) == 0) {
-                if constexpr (MHS_GRP_PAIRS) run_segment_group_pairs<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
-                else run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
-            } else {
-                if constexpr (MHS_GRP_PAIRS) run_segment_group_pairs<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
-                else run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
-            }
+            if (__ballot(n > 0 && L != 3) == 0)
+                run_segment_group<3, RM, true>(f, sb, n, gl, G, a, 3, R, stride);
+            else
+                run_segment_group<3, RM, false>(f, sb, n, gl, G, a, L, R, stride);
         }
     }
 }
@@ -1645,11 +1568,6 @@ __device__ __forceinline__ T ld_idx(const T* __restrict__ base, int i) {
     if constexpr (O32) return *(const T*)((const char*)base + (unsigned)i * (unsigned)sizeof(T));
     else return base[i];
 }
-template <bool O32, class V, class T>
-__device__ __forceinline__ V ld_pair(const T* __restrict__ base, int i) {
-    if constexpr (O32) return *(const V*)((const char*)base + (unsigned)i * (unsigned)sizeof(T));
-    else return *(const V*)(base + i);
-}
 template <bool GM, int MODE, bool O32 = false>
 struct Accum {
     static constexpr bool kValues = true;
@@ -1668,8 +1586,6 @@ struct Accum {
     __device__ __forceinline__ Item load(int i) const { return Item{ld_idx<O32>(Bcol, i), ld_idx<O32>(Bval, i)}; }
     __device__ __forceinline__ int col(int i) const { return ld_idx<O32>(Bcol, i); }
     __device__ __forceinline__ double val(int i) const { return ld_idx<O32>(Bval, i); }
-    __device__ __forceinline__ i2u col2(int i) const { return ld_pair<O32, i2u>(Bcol, i); }
-    __device__ __forceinline__ d2u val2(int i) const { return ld_pair<O32, d2u>(Bval, i); }
     __device__ __forceinline__ void put(const Item& x, double a) const { add(x.c, a * x.v); }
     // acc[column c] += v
     __device__ __forceinline__ void add(int c, double v) const { acc_add<GM>(&acc[index(c)], v); }
@@ -2818,6 +2734,63 @@ struct NumArgs {
     int wave_bytes;          // grouped wave launches: LDS bytes per wave (0: the template's)
 };
 
+// C output of a row (num_row_body, num_row_bitmap): values two a lane, columns four a lane, in
+// 16-byte stores (8-byte aligned doubles and 4-byte aligned ints: gfx950 stores them unaligned);
+// `rank` / `T`: the team's lane and size.  src (LDS) is 16-byte aligned.
+__device__ __forceinline__ void store_vals(double* __restrict__ dst, const double* src, int n, int rank, int T) {
+    for (int r = 2 * rank; r < n; r += 2 * T) {
+        if (r + 1 < n) __builtin_nontemporal_store(*(const d2u*)(src + r), (d2u*)(dst + r));
+        else st_stream(dst + r, src[r]);
+    }
+}
+// the C row's columns (R rows of a group alike) from the staged list cb (LDS, 16-byte aligned)
+__device__ __forceinline__ void store_cols(int* __restrict__ dst, const int* cb, int n, int R, int rank, int T) {
+    for (int r = 4 * rank; r < n; r += 4 * T) {
+        if (r + 3 < n) {
+            const i4a c4 = *(const i4a*)(cb + r);
+            for (int g = 0; g < R; ++g) __builtin_nontemporal_store((i4u)c4, (i4u*)(dst + g * n + r));
+        } else {
+            for (int k = r; k < n; ++k)
+                for (int g = 0; g < R; ++g) st_stream(&dst[g * n + k], cb[k]);
+        }
+    }
+}
+// the columns of a tile table (DIRECT: tile lo + s; hashed: the entry's key) at their C-row ranks
+// into cb: a lane expands a tile of <= 8 columns, a tile of more is expanded by its whole wave
+// (lane = bit, the entry re-read by every lane: a broadcast LDS read)
+template <bool DIRECT>
+__device__ __forceinline__ void stage_cols(const TileEntry* E, int H, int lo, int* cb, int rank, int T) {
+    const int lane = lane_id();
+    for (int s0 = rank & ~63; s0 < H; s0 += T) {
+        const int s = s0 + lane;
+        unsigned long long mk = 0;
+        int key = 0, base = 0;
+        if (s < H) {
+            const TileEntry e = E[s];
+            mk = e.mask;
+            key = DIRECT ? lo + s : e.key;
+            base = e.base;
+        }
+        const bool big = __popcll(mk) > 8;
+        unsigned long long bigs = __ballot(big);
+        if (!big) {
+            int r = base;
+            while (mk) {
+                cb[r++] = (key << TILE_SHIFT) + __builtin_ctzll(mk);
+                mk &= mk - 1;
+            }
+        }
+        while (bigs) {
+            const int src = __builtin_ctzll(bigs);
+            bigs &= bigs - 1;
+            const uint4 q = *reinterpret_cast<const uint4*>(&E[s0 + src]);  // mask, base, key
+            const unsigned long long m2 = ((unsigned long long)q.y << 32) | q.x;
+            const int k2 = DIRECT ? lo + s0 + src : (int)q.w;
+            if ((m2 >> lane) & 1ull) cb[(int)q.z + __popcll(m2 & lanemask_lt())] = (k2 << TILE_SHIFT) + lane;
+        }
+    }
+}
+
 // (forced inline, as num_row: left to the inliner, a grown grouped kernel called them out of
 // line, and the kernel argument they take by reference went to scratch -- 304 bytes a lane,
 // every field read a scratch load)
@@ -3051,116 +3024,20 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
                 }
             }
         }
-    } else if (MHS_OUT_VEC && Team::size == 64) {
-        // wave rows: C.val two a lane and C.col four a lane (16-byte stores: half and a quarter of
-        // the store instructions; the accumulator slices are 16-byte aligned), the columns staged
-        // in LDS by tile (a lane per tile of <= 8 columns, else the wave, lane = bit)
-        const int lane = lane_id();
-        for (int g = 0; g < (GROUPED ? R : 1); ++g) {
-            double* dst = a.Cval + c0 + g * n;
-            const double* src = acc + g * stride;
-            for (int r = 2 * lane; r < n; r += 128) {
-                if (r + 1 < n) __builtin_nontemporal_store(*(const d2u*)(src + r), (d2u*)(dst + r));
-                else st_stream(dst + r, src[r]);
-            }
-        }
-        wave_sync();
-        int* cb = (int*)acc;
-        for (int s0 = 0; s0 < H; s0 += 64) {
-            const int s = s0 + lane;
-            unsigned long long mk = 0;
-            int key = 0, base = 0;
-            if (s < H) {
-                const TileEntry e = E[s];
-                mk = e.mask;
-                key = MODE != NM_HASH ? lo + s : e.key;
-                base = e.base;
-            }
-            const bool big = __popcll(mk) > 8;
-            unsigned long long bigs = __ballot(big);
-            if (!big) {
-                int r = base;
-                while (mk) {
-                    cb[r++] = (key << TILE_SHIFT) + __builtin_ctzll(mk);
-                    mk &= mk - 1;
-                }
-            }
-            while (bigs) {  // the tile's entry re-read by every lane (a broadcast LDS read)
-                const int src = __builtin_ctzll(bigs);
-                bigs &= bigs - 1;
-                const uint4 q = *reinterpret_cast<const uint4*>(&E[s0 + src]);  // mask, base, key
-                const unsigned long long m2 = ((unsigned long long)q.y << 32) | q.x;
-                const int k2 = MODE != NM_HASH ? lo + s0 + src : (int)q.w;
-                if ((m2 >> lane) & 1ull) cb[(int)q.z + __popcll(m2 & lanemask_lt())] = (k2 << TILE_SHIFT) + lane;
-            }
-        }
-        wave_sync();
-        for (int r = 4 * lane; r < n; r += 256) {
-            if (r + 3 < n) {
-                const i4a c4 = *(const i4a*)(cb + r);
-                for (int g = 0; g < (GROUPED ? R : 1); ++g)
-                    __builtin_nontemporal_store((i4u)c4, (i4u*)(a.Ccol + c0 + g * n + r));
-            } else {
-                for (int k = r; k < n; ++k)
-                    for (int g = 0; g < (GROUPED ? R : 1); ++g) st_stream(&a.Ccol[c0 + g * n + k], cb[k]);
-            }
-        }
     } else {
+        // C.val two a lane and C.col four a lane: 16-byte stores, half and a quarter of the store
+        // instructions of one entry a lane (the accumulator slices are 16-byte aligned); the
+        // columns staged in LDS by tile first (a lane per tile of <= 8 columns, else the whole
+        // wave, lane = bit).  Measured (round 4): cant-like numeric -4 %, pwtk- / shipsec1-like
+        // -15 %, hood-like -8 %, cage15-like -7 % -- the walks' loads and the output's stores
+        // share the texture pipeline, which the 8- and 4-byte stores held
         for (int g = 0; g < (GROUPED ? R : 1); ++g)
-            for (int r = tm.rank(); r < n; r += Team::size) st_stream(&a.Cval[c0 + g * n + r], acc[g * stride + r]);
-        if (n >= 8 * t) {
-            // dense masks: one wave per tile, lane = bit
-            const int lane = lane_id();
-            const int nw = Team::size / 64, wv = tm.rank() >> 6;
-            for (int s = wv; s < H; s += nw) {
-                const TileEntry e = E[s];
-                const int key = MODE != NM_HASH ? lo + s : e.key;
-                if (e.mask && ((e.mask >> lane) & 1ull)) {
-                    const int pos = c0 + e.base + __popcll(e.mask & lanemask_lt());
-                    for (int g = 0; g < (GROUPED ? R : 1); ++g) st_part(&a.Ccol[pos + g * n], (key << TILE_SHIFT) + lane);
-                }
-            }
-        } else {
-            // column indices through LDS (the accumulator is free once the values are
-            // out): a lane expands its tile's bits, tiles of more than 8 bits are expanded
-            // by the whole wave (lane = bit); then one coalesced copy to C.col
-            tm.sync();
-            int* cb = (int*)acc;
-            const int lane = lane_id();
-            for (int s0 = tm.rank() & ~63; s0 < H; s0 += Team::size) {
-                const int s = s0 + lane;
-                unsigned long long mk = 0;
-                int key = 0, base = 0;
-                if (s < H) {
-                    const TileEntry e = E[s];
-                    mk = e.mask;
-                    key = MODE != NM_HASH ? lo + s : e.key;
-                    base = e.base;
-                }
-                const bool big = __popcll(mk) > 8;
-                unsigned long long bigs = __ballot(big);
-                if (!big) {
-                    int r = base;
-                    while (mk) {
-                        cb[r++] = (key << TILE_SHIFT) + __builtin_ctzll(mk);
-                        mk &= mk - 1;
-                    }
-                }
-                while (bigs) {  // the tile's entry re-read by every lane (a broadcast LDS read)
-                    const int src = __builtin_ctzll(bigs);
-                    bigs &= bigs - 1;
-                    const uint4 q = *reinterpret_cast<const uint4*>(&E[s0 + src]);  // mask, base, key
-                    const unsigned long long m2 = ((unsigned long long)q.y << 32) | q.x;
-                    const int k2 = MODE != NM_HASH ? lo + s0 + src : (int)q.w;
-                    if ((m2 >> lane) & 1ull) cb[(int)q.z + __popcll(m2 & lanemask_lt())] = (k2 << TILE_SHIFT) + lane;
-                }
-            }
-            tm.sync();
-            for (int r = tm.rank(); r < n; r += Team::size) {
-                const int c = cb[r];
-                for (int g = 0; g < (GROUPED ? R : 1); ++g) st_stream(&a.Ccol[c0 + g * n + r], c);
-            }
-        }
+            store_vals(a.Cval + c0 + g * n, acc + g * stride, n, tm.rank(), Team::size);
+        tm.sync();
+        int* cb = (int*)acc;
+        stage_cols<MODE != NM_HASH>(E, H, lo, cb, tm.rank(), Team::size);
+        tm.sync();
+        store_cols(a.Ccol + c0, cb, n, GROUPED ? R : 1, tm.rank(), Team::size);
     }
     tm.sync();
     MHS_STAMP(5);
@@ -3345,7 +3222,7 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
                   RankAccum<false, O32>{bm, wpre, msk, kb, acc, lo, a.Bcol, a.Bval}, stage);
     tm.sync();
     MHS_STAMP(4);
-    for (int r = tm.rank(); r < n; r += T) st_stream(&a.Cval[c0 + r], acc[r]);
+    store_vals(a.Cval + c0, acc, n, tm.rank(), T);
     tm.sync();  // the accumulator region now stages the column indices
     int* cb = (int*)acc;
     for (int r = tm.rank(); r < t; r += T) {
@@ -3358,7 +3235,7 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
         }
     }
     tm.sync();
-    for (int r = tm.rank(); r < n; r += T) st_stream(&a.Ccol[c0 + r], cb[r]);
+    store_cols(a.Ccol + c0, cb, n, 1, tm.rank(), T);
     tm.sync();
     MHS_STAMP(5);
 }
