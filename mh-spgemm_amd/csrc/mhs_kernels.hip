@@ -747,54 +747,65 @@ __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* 
     bool differ = false;
     int ntiles = 0, prev_col = -1;
     unsigned long long carry = 0;
-    // the next chunk's columns are loaded one iteration ahead (its load latency overlaps
-    // this chunk's shuffles); the chunk-edge neighbour is the next chunk's first column
-    int c_nx = s + gl < e ? col[s + gl] : INT_MAX;
-    int p_nx = (same_len && s + gl < e) ? col[ps + gl] : 0;
-    for (int b = s; b < e; b += G) {
-        const int j = b + gl;
-        const bool in = j < e;
-        const int c = c_nx;
-        if (same_len && in && p_nx != c) differ = true;
-        c_nx = j + G < e ? col[j + G] : INT_MAX;
-        p_nx = (same_len && j + G < e) ? col[ps + (j + G - s)] : 0;
-        const int first_next = __shfl(c_nx, gbase);
-        const int up = __shfl_up(c, 1, G);
-        const int pc = (gl == 0) ? prev_col : up;
-        const int tile = c >> TILE_SHIFT;
-        const int ptile = pc < 0 ? -1 : (pc >> TILE_SHIFT);
-        const bool head = in && tile != ptile;
-        if (in && c < pc) err |= ERR_UNSORTED;
-        if (in && (c < 0 || c >= N)) err |= ERR_COL_RANGE;
-        // next entry's column: within the chunk from the neighbour lane, at the
-        // chunk edge from memory
-        const int dn = __shfl_down(c, 1, G);
-        int nc = (gl == G - 1) ? first_next : dn;
-        if (j + 1 >= e) nc = INT_MAX;
-        const bool tail = in && ((nc >> TILE_SHIFT) != tile || nc == INT_MAX);
-        // forward segmented OR within the chunk
-        unsigned long long m = in ? (1ull << (c & (TILE_BITS - 1))) : 0ull;
-        if (gl == 0 && !head) m |= carry;
+    // MC chunks' columns (and the previous row's, for the same-pattern test) are loaded together,
+    // plus the next group's first chunk (its first column closes the last chunk's runs): one
+    // round trip per MC chunks (cant-like rows of 69 entries in 16-lane groups: 5 chunks, two
+    // round trips instead of five)
+    constexpr int MC = 4;
+    for (int b0 = s; b0 < e; b0 += MC * G) {
+        int cc[MC + 1], pp[MC];
 #pragma unroll
-        for (int d = 1; d < G; d <<= 1) {
-            const unsigned long long om = __shfl_up(m, d, G);
-            const int ot = __shfl_up(tile, d, G);
-            if (gl >= d && ot == tile) m |= om;
+        for (int u = 0; u <= MC; ++u) {
+            const int j = b0 + u * G + gl;
+            cc[u] = j < e ? col[j] : INT_MAX;
+            if (u < MC) pp[u] = (same_len && j < e) ? col[ps + (j - s)] : 0;
         }
-        const unsigned long long hb = __ballot(head) & gmask;
-        if (tail) {
-            const unsigned long long le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
-            const int pos = s + ntiles + __popcll(hb & le) - 1;
-            btcol[pos] = tile;
-            btmask[pos] = m;
+#pragma unroll
+        for (int u = 0; u < MC; ++u) {
+            const int b = b0 + u * G;
+            if (b >= e) break;
+            const int j = b + gl;
+            const bool in = j < e;
+            const int c = cc[u];
+            if (same_len && in && pp[u] != c) differ = true;
+            const int first_next = __shfl(cc[u + 1], gbase);
+            const int up = __shfl_up(c, 1, G);
+            const int pc = (gl == 0) ? prev_col : up;
+            const int tile = c >> TILE_SHIFT;
+            const int ptile = pc < 0 ? -1 : (pc >> TILE_SHIFT);
+            const bool head = in && tile != ptile;
+            if (in && c < pc) err |= ERR_UNSORTED;
+            if (in && (c < 0 || c >= N)) err |= ERR_COL_RANGE;
+            // next entry's column: within the chunk from the neighbour lane, at the
+            // chunk edge from the next chunk's first
+            const int dn = __shfl_down(c, 1, G);
+            int nc = (gl == G - 1) ? first_next : dn;
+            if (j + 1 >= e) nc = INT_MAX;
+            const bool tail = in && ((nc >> TILE_SHIFT) != tile || nc == INT_MAX);
+            // forward segmented OR within the chunk
+            unsigned long long m = in ? (1ull << (c & (TILE_BITS - 1))) : 0ull;
+            if (gl == 0 && !head) m |= carry;
+#pragma unroll
+            for (int d = 1; d < G; d <<= 1) {
+                const unsigned long long om = __shfl_up(m, d, G);
+                const int ot = __shfl_up(tile, d, G);
+                if (gl >= d && ot == tile) m |= om;
+            }
+            const unsigned long long hb = __ballot(head) & gmask;
+            if (tail) {
+                const unsigned long long le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+                const int pos = s + ntiles + __popcll(hb & le) - 1;
+                btcol[pos] = tile;
+                btmask[pos] = m;
+            }
+            ntiles += __popcll(hb);
+            const int last = (e - b < G ? e - b : G) - 1;
+            const unsigned long long lm = __shfl(m, gbase + last);
+            const int lc = __shfl(c, gbase + last);
+            const bool lt = __shfl((int)tail, gbase + last) != 0;
+            carry = lt ? 0ull : lm;
+            prev_col = lc;
         }
-        ntiles += __popcll(hb);
-        const int last = (e - b < G ? e - b : G) - 1;
-        const unsigned long long lm = __shfl(m, gbase + last);
-        const int lc = __shfl(c, gbase + last);
-        const bool lt = __shfl((int)tail, gbase + last) != 0;
-        carry = lt ? 0ull : lm;
-        prev_col = lc;
     }
     const bool same = same_len && (__ballot(differ) & gmask) == 0;
     if (valid && gl == 0) {
@@ -910,7 +921,7 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         // the whole-wave walk of a long row (hub rows of power-law matrices: thousands of
         // entries) takes U entries a lane per round, their loads issued together -- one
         // Acol -> bmeta round trip per U*64 entries instead of per 64
-        constexpr int U = G == 64 ? 4 : 1;
+        constexpr int U = G >= 8 ? 4 : G == 4 ? 2 : 1;  // (round 4: short rows too -- one Acol -> bmeta round trip per U*G entries)
         for (int j0 = s + gl; j0 < e; j0 += G * U) {
             int k[U], kp[U];
             bool in[U];
