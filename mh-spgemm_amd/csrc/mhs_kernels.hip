@@ -728,7 +728,7 @@ __device__ __forceinline__ void acc_add(double* p, double v) {
 // chunk edge is carried in `carry`.  Also checks the sorted-columns precondition.
 // One B row by a lane group of G lanes (every lane of the wave calls it: shuffles and
 // ballots); `valid` false for groups without a row.
-template <int G>
+template <int G, int MC>
 __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* __restrict__ ptr,
                                          const int* __restrict__ col, int* __restrict__ btcol,
                                          unsigned long long* __restrict__ btmask, int4* __restrict__ bmeta,
@@ -749,9 +749,8 @@ __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* 
     unsigned long long carry = 0;
     // MC chunks' columns (and the previous row's, for the same-pattern test) are loaded together,
     // plus the next group's first chunk (its first column closes the last chunk's runs): one
-    // round trip per MC chunks (cant-like rows of 69 entries in 16-lane groups: 5 chunks, two
-    // round trips instead of five)
-    constexpr int MC = 4;
+    // round trip per MC chunks (MC = 4 where rows average more than G entries: wb-edu-like and
+    // cage15-like masks -5..7 %; rows of one chunk keep MC = 1)
     for (int b0 = s; b0 < e; b0 += MC * G) {
         int cc[MC + 1], pp[MC];
 #pragma unroll
@@ -822,7 +821,7 @@ __device__ __forceinline__ void mask_row(int row, bool valid, int N, const int* 
 // walked by the whole wave, one at a time: a G-lane group would hold its wave (and
 // the kernel's tail) for thousands of iterations.
 constexpr int MASK_LONG = 16;
-template <int G>
+template <int G, int MC>
 __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __restrict__ ptr,
                                                 const int* __restrict__ col, int* __restrict__ btcol,
                                                 unsigned long long* __restrict__ btmask,
@@ -835,11 +834,11 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
     int err = 0;
     bool lng = false;
     if constexpr (G < 64) lng = valid && ptr[row + 1] - ptr[row] > MASK_LONG * G;
-    mask_row<G>(row, valid && !lng, N, ptr, col, btcol, btmask, bmeta, bhi, err);
+    mask_row<G, MC>(row, valid && !lng, N, ptr, col, btcol, btmask, bmeta, bhi, err);
     if constexpr (G < 64) {
         for (unsigned long long lb = __ballot(lng && gl == 0); lb; lb &= lb - 1) {
             const int r = __shfl(row, __builtin_ctzll(lb));
-            mask_row<64>(r, true, N, ptr, col, btcol, btmask, bmeta, bhi, err);
+            mask_row<64, 4>(r, true, N, ptr, col, btcol, btmask, bmeta, bhi, err);
         }
     }
     if (__any(err != 0)) {
@@ -897,7 +896,7 @@ __device__ bool last_block_done(int* done) {
 
 // One A row by a group of G lanes (all lanes of the wave call it); returns the row's
 // flop in every lane of the group (0 for invalid groups).
-template <int G>
+template <int G, int U = (G == 64 ? 4 : 1)>
 __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, const int* __restrict__ Aptr,
                                                  const int* __restrict__ Acol, const int4* __restrict__ bmeta,
                                                  const int* __restrict__ bhi, int* __restrict__ rflop,
@@ -918,10 +917,11 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         const int ps = row > 0 ? Aptr[row - 1] : 0;
         differ = !(row > 0 && e > s && s - ps == e - s);
         const int dp = s - ps;
-        // the whole-wave walk of a long row (hub rows of power-law matrices: thousands of
-        // entries) takes U entries a lane per round, their loads issued together -- one
-        // Acol -> bmeta round trip per U*64 entries instead of per 64
-        constexpr int U = G >= 8 ? 4 : G == 4 ? 2 : 1;  // (round 4: short rows too -- one Acol -> bmeta round trip per U*G entries)
+        // U entries a lane per round, their loads issued together -- one Acol -> bmeta round
+        // trip per U*G entries: the whole-wave walk of a long row (hub rows of power-law
+        // matrices: thousands of entries) and the lane groups of matrices whose rows average
+        // more than G entries (round 4: cant-like analysis -15 %, cage15-like -13 %; rows of
+        // fewer entries keep U = 1: delaunay-like +9 % at 4)
         for (int j0 = s + gl; j0 < e; j0 += G * U) {
             int k[U], kp[U];
             bool in[U];
@@ -1016,7 +1016,7 @@ constexpr int AN_LONG = 16;
 // entries (<= 64 rows x 128)
 constexpr int BLK_FLOP_BITS = 40, BLK_SLOT_SHIFT = 48;
 constexpr unsigned long long BLK_FLOP_MASK = (1ull << BLK_FLOP_BITS) - 1;
-template <int G>
+template <int G, int U>
 __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __restrict__ Aptr,
                                                  const int* __restrict__ Acol,
                                                  const int4* __restrict__ bmeta,
@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
     int err = 0, nslots = 0, nother = 0;
     bool lng = false;
     if constexpr (G < 64) lng = valid && Aptr[row + 1] - Aptr[row] > AN_LONG * G;
-    long long flop = analyze_row<G>(row, valid && !lng, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
+    long long flop = analyze_row<G, U>(row, valid && !lng, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
                                     ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig);
     flop = gl == 0 ? flop : 0;
     if constexpr (G < 64) {
@@ -3718,13 +3718,16 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     while (2 * G <= avg / 4 && G < MHS_MASK_GMAX) G <<= 1;
     const int rpb = 256 / G;
     const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
+#define MHS_MASK(GG, MM) hipLaunchKernelGGL((k_mask_b<GG, MM>), grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats)
+    const bool multi = avg > G;  // rows of several chunks: four chunks a round trip
     switch (G) {
-    case 2: hipLaunchKernelGGL(k_mask_b<2>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    case 4: hipLaunchKernelGGL(k_mask_b<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    case 8: hipLaunchKernelGGL(k_mask_b<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    case 16: hipLaunchKernelGGL(k_mask_b<16>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    case 32: hipLaunchKernelGGL(k_mask_b<32>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
-    default: hipLaunchKernelGGL(k_mask_b<64>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats); break;
+    case 2: MHS_MASK(2, 1); break;
+    case 4: MHS_MASK(4, 1); break;
+    case 8: if (multi) MHS_MASK(8, 4); else MHS_MASK(8, 1); break;
+    case 16: if (multi) MHS_MASK(16, 4); else MHS_MASK(16, 1); break;
+    case 32: if (multi) MHS_MASK(32, 4); else MHS_MASK(32, 1); break;
+    default: MHS_MASK(64, 4); break;
+#undef MHS_MASK
     }
 }
 
@@ -3747,14 +3750,17 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG) hipLaunchKernelGGL(k_analyze<GG>, grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr)
+#define MHS_ANALYZE(GG, UU) hipLaunchKernelGGL((k_analyze<GG, UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr)
     switch (G) {
-    case 2: MHS_ANALYZE(2); break;
-    case 4: MHS_ANALYZE(4); break;
-    case 8: MHS_ANALYZE(8); break;
-    case 16: MHS_ANALYZE(16); break;
-    case 32: MHS_ANALYZE(32); break;
-    default: MHS_ANALYZE(64); break;
+    case 2: MHS_ANALYZE(2, 1); break;
+    case 4: MHS_ANALYZE(4, 1); break;
+    case 8:
+        if (A.nnz > 8LL * A.M) MHS_ANALYZE(8, 4);  // rows of more than a group's 8 entries on average
+        else MHS_ANALYZE(8, 1);
+        break;
+    case 16: MHS_ANALYZE(16, 1); break;
+    case 32: MHS_ANALYZE(32, 1); break;
+    default: MHS_ANALYZE(64, 4); break;
     }
 #undef MHS_ANALYZE
     if (w.nft_bin) {  // numeric-first probe: the counts go to the host, which picks the bin lists
