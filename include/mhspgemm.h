@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 7
+#define MHS_ABI_VERSION 8
 
 typedef enum mhs_status {
     MHS_OK = 0,

@@ -414,6 +414,7 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
 // with_near: its phase 0 checks the near row-group candidates (after k_sym_common on the
 // same stream); else launch_near does, once both symbolic launches are done
 void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, bool with_near);
+void launch_symbolic_b256(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s);
 // near row groups: verify k_bin_list's candidates after the symbolic pass, build union rows
 void launch_near(const Csr& A, const Work& w, const int* Cptr, hipStream_t s);
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,

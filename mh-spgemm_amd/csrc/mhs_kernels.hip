@@ -128,7 +128,19 @@ namespace mhs {
 
 // ------------------------------------------------------------------ helpers ---
 
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
+#ifndef MHS_LANE_AVG
+#define MHS_LANE_AVG 9  // k_mask_b / k_analyze: a lane per row below this many entries a row on average (0: off)
+#endif
+#ifndef MHS_OPAQUE_LANE
+#define MHS_OPAQUE_LANE 0  // 1: every lane id recomputed where used (A/B variant)
+#endif
+__device__ __forceinline__ int lane_id() {
+    int l = __lane_id();
+#if MHS_OPAQUE_LANE
+    asm volatile("" : "+v"(l));
+#endif
+    return l;
+}
 
 // Ordering point for LDS traffic between lanes of ONE wave: a wave's LDS
 // operations are performed in issue order, so only the compiler must be kept
@@ -177,8 +189,16 @@ __device__ __forceinline__ long long wave_incl_scan64(long long x) {
     return x;
 }
 
+// threadIdx.x from the wave's index (an SGPR) and the lane: the fused multi-role kernels
+// otherwise keep v0 (the work-item id) live throughout, and at 64 VGPRs spill it
+__device__ __forceinline__ int thread_x() {
+    return (__builtin_amdgcn_readfirstlane((int)threadIdx.x) & ~63) + lane_id();
+}
+// (an opaque lane id: recomputed where used -- hoisted, the mask held two VGPRs across
+// whole kernels, and the 64-VGPR kernels spilled it to scratch)
 __device__ __forceinline__ unsigned long long lanemask_lt() {
-    const int lane = lane_id();
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
@@ -849,6 +869,94 @@ __global__ __launch_bounds__(256) void k_mask_b(int MB, int N, const int* __rest
     }
 }
 
+// Short rows (matrices averaging at most 8 entries a row): a lane per B row, 64 rows a wave.
+// The lane loads U entries of its row at a time (all issued together) and builds the
+// (tile, mask) runs in order in its registers -- no shuffles within a row, so one
+// ptr -> col round trip serves 64 rows instead of the 8-16 of the lane groups (those kernels
+// were bound by that chain: wb-edu-like 0.9 ms, GAP-road-like 0.5 ms for a few hundred MB).
+// Same-pattern test: row r-1 is the lane below (its chunk i sits in the same registers), for
+// lane 0 a load.  Rows past MASK_LANE_LONG entries: whole-wave walks afterwards.
+constexpr int MASK_LANE_LONG = 32;
+template <int U>
+__global__ __launch_bounds__(256) void k_mask_lane(int MB, int N, const int* __restrict__ ptr,
+                                                   const int* __restrict__ col, int* __restrict__ btcol,
+                                                   unsigned long long* __restrict__ btmask,
+                                                   int4* __restrict__ bmeta, int* __restrict__ bhi,
+                                                   Stats* __restrict__ stats) {
+    const int lane = lane_id();
+    const int row = (int)(blockIdx.x * 256u + threadIdx.x);
+    const bool valid = row < MB;
+    const int s = valid ? ptr[row] : 0;
+    const int e = valid ? ptr[row + 1] : 0;
+    const int len = e - s;
+    const bool lng = len > MASK_LANE_LONG;
+    const bool act = valid && !lng && len > 0;
+    // the previous row's length: the lane below's, lane 0 loads it
+    int pl = __shfl_up(len, 1);
+    if (lane == 0) pl = (valid && row > 0) ? s - ptr[row - 1] : -1;
+    const bool same_len = act && row > 0 && pl == len;
+    int err = 0, ntiles = 0, prev_c = -1, cur_t = -1, first_t = INT_MAX;
+    unsigned long long cur_m = 0ull;
+    bool differ = false;
+    const int nch = act ? (len + U - 1) / U : 0;
+    const int maxch = wave_max(nch);  // (uniform trip count: the shuffles need every lane)
+    for (int i = 0; i < maxch; ++i) {
+        int c[U];
+        bool in[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = s + i * U + u;
+            in[u] = act && j < e;
+            c[u] = in[u] ? col[j] : INT_MAX;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int p = __shfl_up(c[u], 1);
+            if (lane == 0 && same_len && in[u]) p = col[s + i * U + u - len];
+            differ = differ || (same_len && in[u] && p != c[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!in[u]) continue;
+            const int cc = c[u];
+            if (cc < prev_c) err |= ERR_UNSORTED;
+            if (cc < 0 || cc >= N) err |= ERR_COL_RANGE;
+            prev_c = cc;
+            const int t = cc >> TILE_SHIFT;
+            if (t != cur_t) {
+                if (cur_t < 0) first_t = t;
+                if (cur_t >= 0) {
+                    btcol[s + ntiles] = cur_t;
+                    btmask[s + ntiles] = cur_m;
+                    ++ntiles;
+                }
+                cur_t = t;
+                cur_m = 0ull;
+            }
+            cur_m |= 1ull << (cc & (TILE_BITS - 1));
+        }
+    }
+    if (cur_t >= 0) {
+        btcol[s + ntiles] = cur_t;
+        btmask[s + ntiles] = cur_m;
+        ++ntiles;
+    }
+    if (valid && !lng) {
+        bmeta[row] = make_int4(s, len, ntiles | (same_len && !differ ? SAME_PATTERN : 0), first_t);
+        bhi[row] = cur_t;  // the last tile (-1: an empty row)
+    }
+    for (unsigned long long lb = __ballot(lng); lb; lb &= lb - 1) {
+        const int r = __shfl(row, __builtin_ctzll(lb));
+        mask_row<64, 4>(r, true, N, ptr, col, btcol, btmask, bmeta, bhi, err);
+    }
+    if (__any(err != 0)) {
+        int werr = err;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) werr |= __shfl_xor(werr, d);
+        if (lane == 0) atomicOr(&stats->err, werr);
+    }
+}
+
 // ------------------------------------------------------------ row analysis ---
 
 __device__ __forceinline__ int sym_bin_of(int flop, int tflop, int span) {
@@ -896,6 +1004,13 @@ __device__ bool last_block_done(int* done) {
 
 // One A row by a group of G lanes (all lanes of the wave call it); returns the row's
 // flop in every lane of the group (0 for invalid groups).
+__device__ __forceinline__ void analyze_out(int row, long long flop, long long tflop, int lo, int hi, int kfirst,
+                                            bool differ, bool bad, int nA, int* __restrict__ rflop,
+                                            int* __restrict__ rtflop, int* __restrict__ rlo, int* __restrict__ rhi,
+                                            int* __restrict__ ctiles, unsigned char* __restrict__ sym_bin,
+                                            int* __restrict__ Cptr, unsigned char* __restrict__ asame,
+                                            unsigned char* __restrict__ nft_bin, int& nslots, int& nother,
+                                            unsigned* __restrict__ nsig);
 template <int G, int U = (G == 64 ? 4 : 1)>
 __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, const int* __restrict__ Aptr,
                                                  const int* __restrict__ Acol, const int4* __restrict__ bmeta,
@@ -969,7 +1084,21 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         const int ob = __shfl_xor((int)bad, d);
         bad = bad || ob != 0;
     }
-    if (valid && gl == 0) {
+    if (valid && gl == 0)
+        analyze_out(row, flop, tflop, lo, hi, kfirst, differ, bad, Aptr[row + 1] - Aptr[row], rflop, rtflop, rlo, rhi,
+                    ctiles, sym_bin, Cptr, asame, nft_bin, nslots, nother, nsig);
+    return valid ? flop : 0;
+}
+
+// A row's analysis outputs (its lane of the group / its own lane).
+__device__ __forceinline__ void analyze_out(int row, long long flop, long long tflop, int lo, int hi, int kfirst,
+                                            bool differ, bool bad, int nA, int* __restrict__ rflop,
+                                            int* __restrict__ rtflop, int* __restrict__ rlo, int* __restrict__ rhi,
+                                            int* __restrict__ ctiles, unsigned char* __restrict__ sym_bin,
+                                            int* __restrict__ Cptr, unsigned char* __restrict__ asame,
+                                            unsigned char* __restrict__ nft_bin, int& nslots, int& nother,
+                                            unsigned* __restrict__ nsig) {
+    {
         // a row with an out-of-range column enters no bin: the symbolic kernels gather
         // bmeta[Acol[j]] unchecked, and the host returns MHS_ERR_INVALID before numeric
         asame[row] = (unsigned char)((differ || bad) ? 0 : 1);
@@ -979,7 +1108,6 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
         rtflop[row] = tf;
         rlo[row] = lo;
         rhi[row] = hi;
-        const int nA = Aptr[row + 1] - Aptr[row];
         const int tc = tiny_class_sym(f, nA);
         const int bin = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
@@ -1005,7 +1133,6 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
             ctiles[row] = 0;
         }
     }
-    return valid ? flop : 0;
 }
 
 // G lanes per A row; rows longer than AN_LONG*G entries are deferred to whole-wave
@@ -1059,6 +1186,100 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
     if (lane == 0) wsum[threadIdx.x >> 6] = mine;
     __syncthreads();
     if (threadIdx.x == 0) blkflop[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (__any(err != 0) && lane == 0) atomicOr(&stats->err, ERR_ACOL_RANGE);
+}
+
+// Short rows (matrices averaging at most 8 entries a row): a lane per A row, 64 rows a wave
+// (as k_mask_lane): the lane loads U of its row's columns at a time, then their bmeta / bhi
+// gathers, all issued together -- one ptr -> Acol -> bmeta chain serves 64 rows.  Rows past
+// AN_LANE_LONG entries: whole-wave walks afterwards.  Two per-block words (128 rows each:
+// the packing of BLK_FLOP_BITS holds at most 255 other rows a word).
+constexpr int AN_LANE_LONG = 32;
+template <int U>
+__global__ __launch_bounds__(256) void k_analyze_lane(int M, int MB, const int* __restrict__ Aptr,
+                                                      const int* __restrict__ Acol, const int4* __restrict__ bmeta,
+                                                      const int* __restrict__ bhi, int* __restrict__ rflop,
+                                                      int* __restrict__ rtflop, int* __restrict__ rlo,
+                                                      int* __restrict__ rhi, int* __restrict__ ctiles,
+                                                      unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
+                                                      unsigned long long* __restrict__ blkflop,
+                                                      unsigned char* __restrict__ asame, Stats* __restrict__ stats,
+                                                      unsigned long long* __restrict__ lb_state, int nlb,
+                                                      unsigned char* __restrict__ nft_bin, unsigned* __restrict__ nsig) {
+    const int lane = lane_id();
+    const int row = (int)(blockIdx.x * 256u + threadIdx.x);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nlb; i += gridDim.x * blockDim.x)
+        lb_state[i] = 0ull;  // k_scan's look-back words (k_scan runs after every analyze block)
+    const bool valid = row < M;
+    int err = 0, nslots = 0, nother = 0;
+    const int s = valid ? Aptr[row] : 0;
+    const int e = valid ? Aptr[row + 1] : 0;
+    const int len = e - s;
+    const bool lng = len > AN_LANE_LONG;
+    const bool act = valid && !lng;
+    int pl = __shfl_up(len, 1);  // the previous row's length: the lane below's, lane 0 loads it
+    if (lane == 0) pl = (valid && row > 0) ? s - Aptr[row - 1] : -1;
+    const bool cmp = act && row > 0 && len > 0 && pl == len;  // compare with row - 1's columns
+    bool differ = !cmp, bad = false;
+    long long flop = 0, tflop = 0;
+    int lo = INT_MAX, hi = -1, kfirst = -1;
+    const int nch = act ? (len + U - 1) / U : 0;
+    const int maxch = wave_max(nch);  // (uniform trip count: the shuffles need every lane)
+    for (int i = 0; i < maxch; ++i) {
+        int k[U];
+        bool in[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = s + i * U + u;
+            in[u] = act && j < e;
+            k[u] = in[u] ? Acol[j] : 0;
+        }
+        int4 m[U];
+        int h[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int kc = in[u] && k[u] >= 0 && k[u] < MB ? k[u] : 0;  // (row 0: a valid slot, unused)
+            m[u] = bmeta[kc];
+            h[u] = bhi[kc];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int p = __shfl_up(k[u], 1);
+            if (lane == 0 && cmp && in[u]) p = Acol[s + i * U + u - len];
+            differ = differ || (in[u] && p != k[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!in[u]) continue;
+            if (i == 0 && u == 0) kfirst = k[u];
+            if (k[u] < 0 || k[u] >= MB) {
+                err = ERR_ACOL_RANGE;
+                bad = true;
+                continue;
+            }
+            flop += m[u].y;
+            tflop += meta_ntiles(m[u]);
+            lo = min(lo, m[u].w);
+            hi = max(hi, h[u]);
+        }
+    }
+    if (act)
+        analyze_out(row, flop, tflop, lo, hi, kfirst, differ, bad, len, rflop, rtflop, rlo, rhi, ctiles, sym_bin,
+                    Cptr, asame, nft_bin, nslots, nother, nsig);
+    if (!act) flop = 0;
+    for (unsigned long long lb = __ballot(lng); lb; lb &= lb - 1) {
+        const int r = __shfl(row, __builtin_ctzll(lb));
+        const long long f = analyze_row<64>(r, true, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles,
+                                            sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig);
+        flop += lane == 0 ? f : 0;
+    }
+    __shared__ unsigned long long wsum[4];
+    unsigned long long mine = (unsigned long long)flop;
+    if (nft_bin) mine += ((unsigned long long)nother << BLK_FLOP_BITS) + ((unsigned long long)nslots << BLK_SLOT_SHIFT);
+    mine = wave_sum(mine);
+    if (lane == 0) wsum[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x < 2) blkflop[2 * blockIdx.x + threadIdx.x] = wsum[2 * threadIdx.x] + wsum[2 * threadIdx.x + 1];
     if (__any(err != 0) && lane == 0) atomicOr(&stats->err, ERR_ACOL_RANGE);
 }
 
@@ -2489,6 +2710,9 @@ __device__ __forceinline__ int block_row_need(bool b1024, int lo, int hi, int t,
                                                              : (int)num_need(span, t, n, dense_span_max);
 }
 
+#ifndef MHS_SCAN_HOIST
+#define MHS_SCAN_HOIST 0  // 1: k_scan's row scalars load with the counts, before the first barrier (measured slower)
+#endif
 template <int PER>
 __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                unsigned long long* __restrict__ state,
@@ -2504,7 +2728,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                long long* __restrict__ tslot, const int* __restrict__ gna,
                                                int4* __restrict__ bmeta_near) {
     constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
-    static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
+    static_assert(PER == 1 || PER == 2 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
     __shared__ long long excl_s;
     __shared__ int bid_s;
@@ -2524,13 +2748,40 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         bid = bid_s;
     }
     const int base = bid * ITEMS + threadIdx.x * PER;
-    int v[PER];
+    // every load of the block's rows issues here, ahead of the first barrier (the classification
+    // below needs none of the prefix): one round trip for the counts and the row scalars
+    unsigned long long fpart = 0;  // the block's share of k_analyze's per-block product partials
+    {
+        const int per = (nflop + (int)gridDim.x - 1) / (int)gridDim.x;
+        const int i1 = min(nflop, (bid + 1) * per);
+        for (int i = bid * per + threadIdx.x; i < i1; i += 1024) fpart += blkflop[i] & BLK_FLOP_MASK;
+    }
+    int v[PER], rlo_k[PER], rhi_k[PER], grp_k[PER], a0_k[PER], a1_k[PER], rfl_k[PER], ctl_k[PER];
+    auto row_scalars = [&]() {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = base + k;
+            const bool in = i < M;
+            rlo_k[k] = in ? rlo[i] : 0;
+            rhi_k[k] = in ? rhi[i] : 0;
+            grp_k[k] = in ? grp[i] : 0;
+            a0_k[k] = in ? Aptr[i] : 0;
+            a1_k[k] = in ? Aptr[i + 1] : 0;
+            rfl_k[k] = in ? rflop[i] : 0;
+            ctl_k[k] = in ? ctiles[i] : 0;
+        }
+    };
     long long loc = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = base + k;
         v[k] = i < M ? Cptr[i] : 0;
         loc += v[k];
+    }
+    if (MHS_SCAN_HOIST) row_scalars();
+    {  // total products (off the tail: the last block only publishes)
+        const unsigned long long f = wave_sum(fpart);
+        if (lane == 0 && f) atomicAdd(&stats->flop, f);
     }
     const long long inc = wave_incl_scan64(loc);
     if (lane == 63) ws[w] = inc;
@@ -2544,17 +2795,9 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     if (threadIdx.x == 0 && bid > 0)
         __hip_atomic_store(&state[bid], LB_AGG | (unsigned long long)total, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    {  // total products: every block adds its share of k_analyze's per-block partials
-       // (off the tail: the last block only publishes)
-        const int per = (nflop + (int)gridDim.x - 1) / (int)gridDim.x;
-        const int i1 = min(nflop, (bid + 1) * per);
-        unsigned long long f = 0;
-        for (int i = bid * per + threadIdx.x; i < i1; i += 1024) f += blkflop[i] & BLK_FLOP_MASK;
-        f = wave_sum(f);
-        if (lane == 0 && f) atomicAdd(&stats->flop, f);
-    }
     // numeric bin of every row (independent of the prefix: its loads overlap the
     // predecessors' publication instead of following the look-back)
+    if (!MHS_SCAN_HOIST) row_scalars();
     __shared__ unsigned char nbin_of[ITEMS];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -2562,9 +2805,9 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         int nbin = NUM_NONE;
         if (i < M) {
             const int n = v[k];
-            const int lo = rlo[i], hi = rhi[i];
+            const int lo = rlo_k[k], hi = rhi_k[k];
             const int span = n ? hi - lo + 1 : 0;
-            int g = grp[i];
+            int g = grp_k[k];
             int hrow = (g & GRP_CONT) ? i - (g & 0x7F) : i;
             int ghd = (g & GRP_CONT) ? grp[hrow] : g;
             if (nonfin && (ghd & GRP_NEAR)) {  // Inf / NaN in B's values: the near group's rows alone
@@ -2580,22 +2823,22 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
             // members decide alike (same C pattern and sizes; flop and A length: the head's)
             // and then stay out
             const int gh = ghd & GRP_RMASK;
-            const int nA = Aptr[i + 1] - Aptr[i];
-            const int hflop = gh > 1 ? rflop[hrow] : rflop[i];
+            const int nA = a1_k[k] - a0_k[k];
+            const int hflop = gh > 1 ? rflop[hrow] : rfl_k[k];
             const int hnA = gh > 1 ? Aptr[hrow + 1] - Aptr[hrow] : nA;
             // tiny sort keys hold the column relative to the row's first tile in 23 bits
             const bool tok = tiny_ok && (long long)span * TILE_BITS - 1 <= TINY_NUM_NMAX;
             // numeric-first rows (k_analyze's rule) have their values: one copy list
-            const int fc = nft && tok ? tiny_class(rflop[i], nA, TINY_SYM_NC) : -1;
+            const int fc = nft && tok ? tiny_class(rfl_k[k], nA, TINY_SYM_NC) : -1;
             const int gb =
-                fc >= 0 ? -1 : num_group_bin_of(n, hflop, span, ctiles[i], gh, dense_span_max, hnA, tok);
+                fc >= 0 ? -1 : num_group_bin_of(n, hflop, span, ctl_k[k], gh, dense_span_max, hnA, tok);
             if (nft && fc < 0) tslot[i] = -1;  // (slot rows: written by the symbolic pass)
             if (gb < 0)
                 nbin = NUM_TINY + fc;
             else if (gb != NUM_NONE)
                 nbin = (g & GRP_CONT) ? NUM_NONE : gb;
             else
-                nbin = num_bin_of(n, rflop[i], span, ctiles[i], &stats->num_global_need, dense_span_max, nA,
+                nbin = num_bin_of(n, rfl_k[k], span, ctl_k[k], &stats->num_global_need, dense_span_max, nA,
                                   tok);
         }
         nbin_of[threadIdx.x * PER + k] = (unsigned char)nbin;
@@ -2604,8 +2847,8 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         {
             int gneed = 0;
             if (nbin == NUM_WSG || nbin == NUM_W16G) {
-                const int gg = grp[i] & GRP_RMASK;
-                gneed = (int)num_need_rows(rhi[i] - rlo[i] + 1, ctiles[i], v[k], dense_span_max, gg > 1 ? gg : 1) +
+                const int gg = grp_k[k] & GRP_RMASK;
+                gneed = (int)num_need_rows(rhi_k[k] - rlo_k[k] + 1, ctl_k[k], v[k], dense_span_max, gg > 1 ? gg : 1) +
                         WAVE_HDR;
             }
             // (LDS first: one global atomic per wave measured +10 us on cant-like's k_scan --
@@ -2620,7 +2863,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         // CU than a fixed 64 / 157 KiB when the rows are smaller)
         int need = 0;
         if (nbin == NUM_B256 || nbin == NUM_B1024)
-            need = block_row_need(nbin == NUM_B1024, rlo[i], rhi[i], ctiles[i], v[k], dense_span_max);
+            need = block_row_need(nbin == NUM_B1024, rlo_k[k], rhi_k[k], ctl_k[k], v[k], dense_span_max);
         const int n256 = wave_max(nbin == NUM_B256 ? need : 0), n1024 = wave_max(nbin == NUM_B1024 ? need : 0);
         if (n256 | n1024) {  // the split launches (B256_SPLIT / B1024_SPLIT)
             const int split = nbin == NUM_B256 ? B256_SPLIT : B1024_SPLIT;
@@ -3420,11 +3663,6 @@ struct TinyArgs {
 template <int W, int K, bool NUMERIC>
 __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
     static_assert((W & (W - 1)) == 0 && W <= 64 && (K & (K - 1)) == 0 && W * K <= (1 << TINY_EBITS), "team shape");
-    const int lane = lane_id();
-    const int tl = lane & (W - 1);   // lane in the team
-    const int tb = lane & ~(W - 1);  // the team's first lane
-    const unsigned long long tmask = W == 64 ? ~0ull : (((1ull << (W & 63)) - 1) << tb);
-    const unsigned long long below = tmask & lanemask_lt();
     const int count = a.count >= 0 ? a.count : a.stats->sym_count[a.bin];
     const bool slots = NUMERIC && a.sc_col != nullptr;  // numeric-first: into value slots
     const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W), bid, nb);
@@ -3432,6 +3670,14 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
     double* vstage = (double*)tiny_smem + (size_t)(threadIdx.x / W) * (W * K);  // numeric: W*K doubles per team
     // the wave iterates while any of its teams has a row (shuffles need every lane)
     for (int it = rw.first; __ballot(it < rw.end) != 0; it += rw.stride) {
+        // the lane's team masks, rebuilt every row from an opaque lane id: hoisted, they stayed
+        // live across the fused kernels' class dispatch and went to scratch (64-VGPR budget)
+        int lane = lane_id();
+        asm volatile("" : "+v"(lane));
+        const int tl = lane & (W - 1);   // lane in the team
+        const int tb = lane & ~(W - 1);  // the team's first lane
+        const unsigned long long tmask = W == 64 ? ~0ull : (((1ull << (W & 63)) - 1) << tb);
+        const unsigned long long below = tmask & (lane == 0 ? 0ull : (~0ull >> (64 - lane)));
         const bool live = it < rw.end;
         const int row = live ? a.list[it] : 0;
         const int a0 = live ? a.Aptr[row] : 0, nA = live ? a.Aptr[row + 1] - a0 : 0;
@@ -3687,7 +3933,11 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_common(Sy
 #ifndef MHS_SCAN_BIG_M
 #define MHS_SCAN_BIG_M (1 << 19)
 #endif
-static int scan_per(int M) { return M >= MHS_SCAN_BIG_M ? 4 : 1; }
+#ifndef MHS_SCAN_PER
+#define MHS_SCAN_PER 4  // k_scan's rows per thread for big M (1, 2 or 4)
+#endif
+static int scan_per(int M) { return M >= MHS_SCAN_BIG_M ? MHS_SCAN_PER : 1; }
+static int bin_list_per(int M) { return M >= MHS_SCAN_BIG_M ? 4 : 1; }
 
 #ifndef MHS_ROW_GMIN
 #define MHS_ROW_GMIN 4  // narrowest lane group per row in k_mask_b / k_analyze (tiny rows: 16 per wave)
@@ -3713,6 +3963,14 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
     // about four chunk iterations per row: a wave then holds several rows, whose
     // dependent load chains overlap (measured on gfx950: 64-lane rows were latency-bound)
     const long long avg = B.M > 0 ? B.nnz / B.M : 0;
+    if (avg < MHS_LANE_AVG) {  // short rows: a lane per row
+        const dim3 grid((B.M + 255) / 256), blk(256);
+        if (avg < 4)
+            hipLaunchKernelGGL(k_mask_lane<4>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats);
+        else
+            hipLaunchKernelGGL(k_mask_lane<8>, grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats);
+        return;
+    }
     // rows of < 3 entries (road networks): 2-lane groups, 32 rows per wave (GAP-road-like -3.6 %)
     int G = avg < 3 ? 2 : avg < 4 ? MHS_ROW_GMIN : 8;
     while (2 * G <= avg / 4 && G < MHS_MASK_GMAX) G <<= 1;
@@ -3733,16 +3991,18 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
 
 // k_analyze: G lanes per row, 256-thread blocks.
 // 2-lane groups for rows of < 3 entries on average (GAP-road-like 5.29 -> 4.97 ms)
+// G = 1: k_analyze_lane (rows averaging fewer than MHS_LANE_AVG entries; two per-block words)
 static void analyze_geometry(long long nnzA, int M, int* G, int* blocks) {
-    *G = M > 0 && nnzA / M < 3 ? 2 : pick_group(nnzA, M, MHS_AN_GMAX);
+    const long long avg = M > 0 ? nnzA / M : 0;
+    *G = avg < MHS_LANE_AVG ? 1 : avg < 3 ? 2 : pick_group(nnzA, M, MHS_AN_GMAX);
     const int rpb = 256 / *G;
     *blocks = (M + rpb - 1) / rpb;
 }
 
-int analyze_blocks(long long nnzA, int M) {
+int analyze_blocks(long long nnzA, int M) {  // k_analyze's per-block words
     int G, blocks;
     analyze_geometry(nnzA, M, &G, &blocks);
-    return blocks;
+    return G == 1 ? 2 * blocks : blocks;
 }
 
 void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cptr, Published* pub, int seq) {
@@ -3751,7 +4011,12 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
 #define MHS_ANALYZE(GG, UU) hipLaunchKernelGGL((k_analyze<GG, UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr)
+#define MHS_ANALYZE_LANE(UU) hipLaunchKernelGGL((k_analyze_lane<UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr)
     switch (G) {
+    case 1:
+        if (A.nnz < 4LL * A.M) MHS_ANALYZE_LANE(4);
+        else MHS_ANALYZE_LANE(8);
+        break;
     case 2: MHS_ANALYZE(2, 1); break;
     case 4: MHS_ANALYZE(4, 1); break;
     case 8:
@@ -3763,8 +4028,10 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     default: MHS_ANALYZE(64, 4); break;
     }
 #undef MHS_ANALYZE
+#undef MHS_ANALYZE_LANE
     if (w.nft_bin) {  // numeric-first probe: the counts go to the host, which picks the bin lists
-        hipLaunchKernelGGL(k_probe_publish, dim3(64), dim3(1024), 0, s, (const unsigned long long*)w.blkflop, blocks,
+        hipLaunchKernelGGL(k_probe_publish, dim3(64), dim3(1024), 0, s, (const unsigned long long*)w.blkflop,
+                           G == 1 ? 2 * blocks : blocks,
                            w.stats, pub, seq);
         return;
     }
@@ -3774,7 +4041,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
 void launch_bin_list(const Csr& A, const Work& w, hipStream_t s) {
     const unsigned char* nb = w.nft ? w.nft_bin : nullptr;
     const NearCand nc{w.nsig, (w.groups && !nb) ? w.near_list : nullptr};
-    if (scan_per(A.M) == 4)
+    if (bin_list_per(A.M) == 4)
         hipLaunchKernelGGL(k_bin_list<4>, dim3((A.M + 4095) / 4096), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
                            w.groups, w.bin_list, nb, w.stats, nc);
     else
@@ -3958,6 +4225,14 @@ void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, 
     SymArgs a = sym_args(A, w, M, N, Cptr);
     const NearArgs np = with_near ? near_args(A, w, Cptr) : NearArgs{};
     hipLaunchKernelGGL(k_sym_rare, dim3(256), dim3(1024), LDS_MAX - 1024, s, a, np);
+}
+
+// The 32 KiB block bin (its own launch: at one block per CU in k_sym_rare it would hold a fifth
+// of the rows in flight).  With the rare bins on an aux stream it follows the common bins on the
+// call's stream, beside k_sym_rare (webbase-like: 60 us off the symbolic phase).
+void launch_symbolic_b256(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s) {
+    if (M <= 0) return;
+    SymArgs a = sym_args(A, w, M, N, Cptr);
     a.bin = SYM_B256;
     hipLaunchKernelGGL((k_sym_block<256, false>), dim3(round8(M, MHS_SYM_B256_GRID)), dim3(256), SYM_B256_BYTES, s, a);
 }
@@ -3971,6 +4246,7 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
                        w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
                        w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, w.gna, w.near_b ? w.bmeta : nullptr)
     if (per == 4) MHS_SCAN(4);
+    else if (per == 2) MHS_SCAN(2);
     else MHS_SCAN(1);
 #undef MHS_SCAN
 }
