@@ -48,7 +48,6 @@ struct mhs_ctx {
     long long ncalls = 0;
     int mc_list = 0;         // tile-list cap of the row cache (0: mc_list_for(M); MHS_MC_LIST)
     bool stats_zero = false; // the workspace's device Stats are zero (left so by the last k_scan)
-    bool preforked = false;  // the aux streams already wait for this call's k_scan (pre_fork)
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     bool tiny_num = true;    // numeric tiny (sort) classes (MHS_NO_TINY_NUM=1: off)
     // numeric-first tiny rows from this many rows of A on (MHS_OPT_TINY_FIRST_ROWS,
@@ -354,22 +353,6 @@ constexpr int NUM_GLOBAL_GRID = 128;
 
 // The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
 // the aux streams, which join the call's stream again.
-// The aux streams' wait for k_scan, enqueued while k_scan runs (before the host's wait for its
-// Stats): the numeric launches after the hand-off then start without the fork's API calls
-// (a record and three waits: ~10-20 us of host time on the critical path of small products).
-// An aux stream not used by the call just passes the wait.
-#ifndef MHS_PREFORK
-#define MHS_PREFORK 1
-#endif
-int pre_fork(mhs_ctx* ctx) {
-    ctx->preforked = false;
-    if (!MHS_PREFORK || ctx->num_streams <= 1 || !ctx->aux[0]) return MHS_OK;
-    MHS_HIP(hipEventRecord(ctx->fork_ev, ctx->stream));
-    for (int i = 0; i + 1 < ctx->num_streams; ++i) MHS_HIP(hipStreamWaitEvent(ctx->aux[i], ctx->fork_ev, 0));
-    ctx->preforked = true;
-    return MHS_OK;
-}
-
 int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out) {
     hipStream_t s = ctx->stream;
     // several heavy bins: deal them over the aux streams (fork/join costs ~10-20 us,
@@ -378,15 +361,12 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     const int nl = numeric_launches(h);
     const int nss = (nl >= 3 && h.flop >= (1ull << MHS_MULTI_FLOP_LOG2)) ? std::min(ctx->num_streams, nl) : 1;
     if (nss > 1) {
-        // forked before the hand-off unless work went onto the call's stream since (the union copy)
-        const bool fork = !ctx->preforked || w.bx_on;
-        if (fork) MHS_HIP(hipEventRecord(ctx->fork_ev, s));
+        MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         for (int i = 1; i < nss; ++i) {
             ss[i] = ctx->aux[i - 1];
-            if (fork) MHS_HIP(hipStreamWaitEvent(ss[i], ctx->fork_ev, 0));
+            MHS_HIP(hipStreamWaitEvent(ss[i], ctx->fork_ev, 0));
         }
     }
-    ctx->preforked = false;
     // block bins split by LDS need only where their two launches can run side by side (on
     // one stream the hub rows' launch would no longer overlap the others' bulk).  The partition
     // runs on the call's stream after the fork: only the split launches wait for it (split_ev),
@@ -817,11 +797,6 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
         MHS_HIP(hipGetLastError());
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
-        rc = pre_fork(ctx);
-        if (rc) {
-            pool_put(ctx, out.ptr);
-            return rc;
-        }
         rc = wait_published(ctx, s, ctx->pub, seq);
         if (rc) {
             pool_put(ctx, out.ptr);
