@@ -128,6 +128,9 @@ namespace mhs {
 
 // ------------------------------------------------------------------ helpers ---
 
+#ifndef MHS_SYM_PREFETCH
+#define MHS_SYM_PREFETCH 1  // symbolic wave rows: the next 64 rows' scalars in one batch
+#endif
 #ifndef MHS_LANE_AVG
 #define MHS_LANE_AVG 9  // k_mask_b / k_analyze: a lane per row below this many entries a row on average (0: off)
 #endif
@@ -2051,12 +2054,27 @@ struct SymTileBuild {
     }
 };
 
+// A symbolic row's scalars (loaded in the row, or batch-prefetched by sym_wave_rows)
+struct SymRow {
+    int row, lo, hi, tflop, a0, a1;
+};
 template <class Team>
-__device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E, int4* stage) {
-    const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
-    const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
+__device__ void sym_row_s(const Team& tm, const SymArgs& a, const SymRow& r, TileEntry* E, int4* stage);
+template <class Team>
+__device__ __forceinline__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E, int4* stage) {
+    SymRow r;
+    r.row = row;
+    r.lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
+    r.hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
+    r.tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
+    r.a0 = __builtin_amdgcn_readfirstlane(a.Aptr[row]);
+    r.a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
+    sym_row_s(tm, a, r, E, stage);
+}
+template <class Team>
+__device__ void sym_row_s(const Team& tm, const SymArgs& a, const SymRow& r, TileEntry* E, int4* stage) {
+    const int row = r.row, lo = r.lo, hi = r.hi, tflop = r.tflop;
     const int span = hi - lo + 1;
-    const int tflop = __builtin_amdgcn_readfirstlane(a.rtflop[row]);
     const bool direct = sym_direct(span, tflop);
     const int H = direct ? span : hash_slots(tflop < span ? tflop : span);
     unsigned long long* Mk = reinterpret_cast<unsigned long long*>(E);
@@ -2066,9 +2084,8 @@ __device__ void sym_row(const Team& tm, const SymArgs& a, int row, TileEntry* E,
         if (!direct) Kk[s] = -1;
     }
     tm.sync();
-    walk_products(tm, __builtin_amdgcn_readfirstlane(a.Aptr[row]), __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]),
-                  a.Acol, nullptr, a.bmeta, true, tflop, SymTileBuild{Mk, Kk, direct, lo, H, a.btcol, a.btmask},
-                  stage);
+    walk_products(tm, r.a0, r.a1, a.Acol, nullptr, a.bmeta, true, tflop,
+                  SymTileBuild{Mk, Kk, direct, lo, H, a.btcol, a.btmask}, stage);
     tm.sync();
     long long n = 0;
     int t = 0;
@@ -2154,8 +2171,33 @@ __device__ __forceinline__ void sym_wave_rows(const SymArgs& a, int bid, int nb)
     const int count = a.stats->sym_count[a.bin];
     const int* list = a.list + (long long)(a.bin - 1) * a.M;
     WaveTeam tm;
+#if MHS_SYM_PREFETCH
+    // the wave's next 64 rows and their scalars in one batch (lane j: the row at step j), read
+    // back with readlane: the list -> row scalars round trips leave the rows' chains
+    const int lane = lane_id();
+    const RowWalk rw(count, WPB, w, bid, nb);
+    for (int b0 = rw.first; b0 < rw.end; b0 += 64 * rw.stride) {
+        const int li = b0 + lane * rw.stride;
+        const bool in = li < rw.end;
+        const int row = in ? list[li] : 0;
+        const int lo = in ? a.rlo[row] : 0, hi = in ? a.rhi[row] : 0, tf = in ? a.rtflop[row] : 0;
+        const int a0 = in ? a.Aptr[row] : 0, a1 = in ? a.Aptr[row + 1] : 0;
+        const int nrows = min(64, (rw.end - b0 + rw.stride - 1) / rw.stride);
+        for (int j = 0; j < nrows; ++j) {
+            SymRow r;
+            r.row = __builtin_amdgcn_readlane(row, j);
+            r.lo = __builtin_amdgcn_readlane(lo, j);
+            r.hi = __builtin_amdgcn_readlane(hi, j);
+            r.tflop = __builtin_amdgcn_readlane(tf, j);
+            r.a0 = __builtin_amdgcn_readlane(a0, j);
+            r.a1 = __builtin_amdgcn_readlane(a1, j);
+            sym_row_s(tm, a, r, E, nullptr);
+        }
+    }
+#else
     for (RowWalk rw(count, WPB, w, bid, nb); rw.first < rw.end; rw.first += rw.stride)
         sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, nullptr);
+#endif
 }
 
 template <int T, bool GLOBALMEM>
@@ -3501,17 +3543,31 @@ enum NumModes : int { MODES_ALL = 0, MODES_NOHASH = 1, MODES_HASH = 2 };
 
 // Row-level scalars are made provably wave-uniform (readfirstlane) so that the
 // mode dispatch and every per-row loop bound compile to scalar control flow.
+struct NumRow {
+    int row, lo, hi, t, c0, n, a0, a1;
+};
+template <class Team, bool GLOBALMEM, bool GROUPED = false, int MODES = MODES_ALL, bool O32 = false>
+__device__ __forceinline__ void num_row_s(const Team& tm, const NumArgs& a, const NumRow& r, char* region,
+                                          int* counter, int4* stage, int R = 1);
 template <class Team, bool GLOBALMEM, bool GROUPED = false, int MODES = MODES_ALL, bool O32 = false>
 __device__ __forceinline__ void num_row(const Team& tm, const NumArgs& a, int row, char* region, int* counter,
                         int4* stage, int R = 1) {
-    const int lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
-    const int hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
+    NumRow r;
+    r.row = row;
+    r.lo = __builtin_amdgcn_readfirstlane(a.rlo[row]);
+    r.hi = __builtin_amdgcn_readfirstlane(a.rhi[row]);
+    r.t = __builtin_amdgcn_readfirstlane(a.ctiles[row]);
+    r.c0 = __builtin_amdgcn_readfirstlane(a.Cptr[row]);
+    r.n = __builtin_amdgcn_readfirstlane(a.Cptr[row + 1]) - r.c0;
+    r.a0 = __builtin_amdgcn_readfirstlane(a.Aptr[row]);
+    r.a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
+    num_row_s<Team, GLOBALMEM, GROUPED, MODES, O32>(tm, a, r, region, counter, stage, R);
+}
+template <class Team, bool GLOBALMEM, bool GROUPED, int MODES, bool O32>
+__device__ __forceinline__ void num_row_s(const Team& tm, const NumArgs& a, const NumRow& r, char* region,
+                                          int* counter, int4* stage, int R) {
+    const int row = r.row, lo = r.lo, hi = r.hi, t = r.t, c0 = r.c0, n = r.n, a0 = r.a0, a1 = r.a1;
     const int span = hi - lo + 1;
-    const int t = __builtin_amdgcn_readfirstlane(a.ctiles[row]);
-    const int c0 = __builtin_amdgcn_readfirstlane(a.Cptr[row]);
-    const int n = __builtin_amdgcn_readfirstlane(a.Cptr[row + 1]) - c0;
-    const int a0 = __builtin_amdgcn_readfirstlane(a.Aptr[row]);
-    const int a1 = __builtin_amdgcn_readfirstlane(a.Aptr[row + 1]);
     const int mode = num_mode(span, t, n, a.dense_span_max);
     if constexpr (MODES == MODES_HASH) {
         num_row_body<Team, GLOBALMEM, NM_HASH, GROUPED, O32>(tm, a, row, lo, span, t, c0, n, a0, a1, region, counter, stage, R);
