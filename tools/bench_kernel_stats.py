@@ -2,7 +2,7 @@
 run: bench.py times the headline matrix first (warmup + steps pipelined calls, then 5 synchronised
 phase calls and one cold call) and the configs block after it, so the rocprof --stats file mixes
 the configs' launches of the same kernels into its averages.  This splits the kernel trace at the
-first k_mask_b launch past the headline's calls and writes rocprof-style stats of each part.
+first mask launch (k_mask_b / k_mask_lane) past the headline's calls and writes rocprof-style stats of each part.
 
   python tools/bench_kernel_stats.py <kernel_trace.csv> <out_dir> [warmup steps]
 """
@@ -20,7 +20,7 @@ def main():
     calls = warmup + steps + 5 + 1  # pipelined + phase calls + cold call
     seen, cut = 0, len(rows)
     for i, r in enumerate(rows):
-        if "k_mask_b" in r["Kernel_Name"]:
+        if "k_mask_" in r["Kernel_Name"]:  # k_mask_b or k_mask_lane
             seen += 1
             if seen == calls + 1:
                 cut = i

@@ -23,6 +23,8 @@ CALLS = 5  # tools/sweep.py --reps 2: 3 warm-up + 2 timed calls
 # kernel (demangled prefix) -> bin class (include/mhspgemm.h sym_bins / num_bins)
 CLASSES = [
     ("k_mask_b", "front: Form_mask_matrix_B"),
+    ("k_mask_lane", "front: Form_mask_matrix_B (a lane per row)"),
+    ("k_analyze_lane", "front: row analysis (a lane per row)"),
     ("k_analyze", "front: row analysis (symbolic binning)"),
     ("k_probe_publish", "front: numeric-first probe"),
     ("k_bin_list", "front: symbolic bin lists"),
@@ -47,7 +49,7 @@ CLASSES = [
 
 
 def short(name: str) -> str:
-    n = name.replace("void ", "").replace("mhs::", "")
+    n = name.replace("void ", "").replace("mhs::", "").replace("(anonymous namespace)::", "")
     return n.split("(")[0]
 
 

@@ -2,7 +2,7 @@
 usage: python tools/timeline.py gpurun_out/<dir>/run_kernel_trace.csv [first-kernel-substring]"""
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
-first = sys.argv[2] if len(sys.argv) > 2 else "k_mask_b"
+first = sys.argv[2] if len(sys.argv) > 2 else "k_mask_"  # k_mask_b or k_mask_lane
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
 st, en = idx[-3], idx[-2]
