@@ -131,9 +131,6 @@ namespace mhs {
 #ifndef MHS_SYM_PREFETCH
 #define MHS_SYM_PREFETCH 1  // symbolic wave rows: the next 64 rows' scalars in one batch
 #endif
-#ifndef MHS_HUB_DEAL
-#define MHS_HUB_DEAL 0  // numeric hub-row launches first on streams of their own (1, 2; 0: round robin)
-#endif
 #ifndef MHS_LANE_AVG
 #define MHS_LANE_AVG 9  // k_mask_b / k_analyze: a lane per row below this many entries a row on average (0: off)
 #endif
@@ -4410,7 +4407,6 @@ bool launch_split_bins(const Work& w, const Stats& h, int M, const int* Cptr, hi
 namespace {
 struct NumLaunch {
     std::function<void(hipStream_t)> go;
-    bool hub = false;  // a block bin's rows past its LDS split (the split's hub-row launch)
 };
 }  // namespace
 
@@ -4534,7 +4530,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             const int big = h.num_block_big[k];
             const int* l = w.split_list + (k ? 0 : (h.num_count[NUM_B1024] > 0 ? h.num_count[NUM_B1024] : 0));
             go(l + (count - big), big, block_lds(h.num_block_need[k], budget, T), big_slot, split_ev);
-            L.back().hub = true;
             go(l, count - big, block_lds(h.num_block_small_need[k], budget, T), bin, split_ev);
         } else {
             go(w.bin_list + (long long)(bin - 1) * A.M, count, block_lds(h.num_block_need[k], budget, T), bin, nullptr);
@@ -4643,33 +4638,6 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     int used = 0;
     const int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
-#if MHS_HUB_DEAL
-    // the split block bins' hub-row launches (the calls' longest: one heavy row a block) first, each
-    // on an aux stream of its own; then the rest in order, round robin -- over the other streams
-    // (MHS_HUB_DEAL 1) or over all of them after the hubs (2)
-    int nh = 0;
-    for (const NumLaunch& x : L) nh += x.hub;
-    if (n > 1 && nh > 0 && nh < n) {
-        int k = 1;
-        for (NumLaunch& x : L)
-            if (x.hub) {
-                used |= 1 << k;
-                x.go(ss[k++]);
-            }
-        int others[8], no = 0;  // mode 1: the streams without a hub launch (aux ones first)
-        for (int j = nh + 1; j < n; ++j) others[no++] = j;
-        others[no++] = 0;
-        int i = 0;
-        for (NumLaunch& x : L)
-            if (!x.hub) {
-                const int ks = MHS_HUB_DEAL == 1 ? others[i % no] : (nh + 1 + i) % n;
-                used |= 1 << ks;
-                x.go(ss[ks]);
-                ++i;
-            }
-        return used;
-    }
-#endif
     for (size_t i = 0; i < L.size(); ++i) {
         const int k = n > 1 ? (int)((i + 1) % n) : 0;
         used |= 1 << k;
