@@ -54,6 +54,9 @@ struct mhs_ctx {
     // MHS_NFT_MIN_M; < 0: never): one hand-off more per call, so big matrices only
     long long nft_min_m = 1 << 19;
     bool sym_fork = false;   // MHS_SYM_FORK=1: rare symbolic bins on an aux stream for every call
+    // ... and for every call of at least this many rows (MHS_SYM_FORK_MIN_M; < 0: never): the
+    // fork's cross-stream wait (~20 us) is noise there, the rare bins' milliseconds are not
+    long long sym_fork_min_m = 1 << 19;
     bool nft_slots = true;   // MHS_NFT_NO_SLOTS=1 (tests): count the rows only, as when the slots do not fit
     int nft_other_pct = 5;   // slots only when at most this share of the rows is past the tiny classes (MHS_NFT_OTHER_PCT)
     char* slots = nullptr;   // their value slots (cached across calls)
@@ -588,6 +591,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_NFT_MIN_M")) ctx->nft_min_m = atoll(e);
     if (getenv("MHS_NFT_NO_SLOTS")) ctx->nft_slots = false;
     if (const char* e = getenv("MHS_SYM_FORK")) ctx->sym_fork = atoi(e) != 0;
+    if (const char* e = getenv("MHS_SYM_FORK_MIN_M")) ctx->sym_fork_min_m = atoll(e);
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     *out = ctx;
     return MHS_OK;
@@ -772,7 +776,8 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // persistent grids that read their bins' sizes on the device: no host round trip.
     // Numeric-first: rows of the rare bins (long, few) run on an aux stream beside the
     // common bins -- their tail no longer idles the chip
-    if (((w.nft && other > 0) || ctx->sym_fork) && ctx->num_streams > 1 && ctx->aux[0]) {
+    const bool fork_big = ctx->sym_fork_min_m >= 0 && M >= ctx->sym_fork_min_m;
+    if (((w.nft && other > 0) || ctx->sym_fork || fork_big) && ctx->num_streams > 1 && ctx->aux[0]) {
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
         launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0], false);
