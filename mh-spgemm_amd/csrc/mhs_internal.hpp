@@ -68,7 +68,10 @@ constexpr int TINY_FUSED_KMAX = 4;  // largest K of the numeric classes 0..3 (on
 // would not fit the small wave bin (measured: cop20k-like 2.3x slower sorted, while
 // rows that need big tables run 2x faster sorted).
 constexpr int TINY_SYM_NC = 4;
-constexpr int TINY_NUM_SMALL = 4;  // numeric classes >= this only replace big-table rows
+#ifndef MHS_TINY_NUM_SMALL
+#define MHS_TINY_NUM_SMALL 4
+#endif
+constexpr int TINY_NUM_SMALL = MHS_TINY_NUM_SMALL;  // numeric classes >= this only replace big-table rows
 __host__ __device__ inline int tiny_class(int flop, int nA, int nc = TINY_NC) {
     if (flop <= 0) return -1;
     for (int c = 0; c < nc; ++c)

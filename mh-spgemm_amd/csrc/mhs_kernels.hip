@@ -131,6 +131,12 @@ namespace mhs {
 #ifndef MHS_SYM_PREFETCH
 #define MHS_SYM_PREFETCH 1  // symbolic wave rows: the next 64 rows' scalars in one batch
 #endif
+#ifndef MHS_TINY_DUP
+#define MHS_TINY_DUP 2  // ... and at most this many products a C column
+#endif
+#ifndef MHS_TINY_SPARSE_PCT
+#define MHS_TINY_SPARSE_PCT 50  // class-4 rows with tiles >= this % of their C columns go to the sort class (0: off)
+#endif
 #ifndef MHS_LANE_AVG
 #define MHS_LANE_AVG 9  // k_mask_b / k_analyze: a lane per row below this many entries a row on average (0: off)
 #endif
@@ -2709,6 +2715,11 @@ __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int*
     if (n == 0) return NUM_NONE;
     const int tc = tiny_ok ? tiny_class(flop, nA) : -1;
     if (tc >= 0 && tc < TINY_NUM_SMALL) return NUM_TINY + tc;
+    // scattered rows of the first 64-lane class (about a tile per C column: their tables cost a
+    // tile, a hash probe and a rank per column) with few repeated columns sort in registers too
+    if (MHS_TINY_SPARSE_PCT > 0 && tc == TINY_NUM_SMALL && 100LL * t >= (long long)MHS_TINY_SPARSE_PCT * n &&
+        (long long)MHS_TINY_DUP * n >= flop)
+        return NUM_TINY + tc;
     const long long need = num_need(span, t, n, dense_span_max);
     const bool hash = num_mode(span, t, n, dense_span_max) == NM_HASH;
     if (need <= NUM_WS_BYTES - WAVE_HDR && flop <= NUM_WS_WORK) return hash ? NUM_WSH : NUM_WS;
