@@ -128,9 +128,6 @@ namespace mhs {
 
 // ------------------------------------------------------------------ helpers ---
 
-#ifndef MHS_SYM_PREFETCH
-#define MHS_SYM_PREFETCH 1  // symbolic wave rows: the next 64 rows' scalars in one batch
-#endif
 #ifndef MHS_TINY_DUP
 #define MHS_TINY_DUP 2  // ... and at most this many products a C column
 #endif
@@ -140,16 +137,7 @@ namespace mhs {
 #ifndef MHS_LANE_AVG
 #define MHS_LANE_AVG 9  // k_mask_b / k_analyze: a lane per row below this many entries a row on average (0: off)
 #endif
-#ifndef MHS_OPAQUE_LANE
-#define MHS_OPAQUE_LANE 0  // 1: every lane id recomputed where used (A/B variant)
-#endif
-__device__ __forceinline__ int lane_id() {
-    int l = __lane_id();
-#if MHS_OPAQUE_LANE
-    asm volatile("" : "+v"(l));
-#endif
-    return l;
-}
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Ordering point for LDS traffic between lanes of ONE wave: a wave's LDS
 // operations are performed in issue order, so only the compiler must be kept
@@ -1485,9 +1473,6 @@ __device__ __forceinline__ void wave_chunks(int jb0, int jstep, int a1, const in
 
 // A wave's row walk with chunks staged in pairs (as for_products_group) and a lane-group
 // width per chunk (chunk_group): a row's short last chunk takes wide groups.
-#ifndef MHS_WAVE_PAIRS
-#define MHS_WAVE_PAIRS 1
-#endif
 template <class F>
 __device__ __forceinline__ void wave_walk(int a0, int a1, const int* __restrict__ Acol, const double* __restrict__ Aval,
                                           const int4* __restrict__ bmeta, bool tiles, long long work, const F& f) {
@@ -1750,7 +1735,7 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
                                               const int4* __restrict__ bmeta, bool tiles,
                                               long long work, const F& f, int4* stage) {
     const int nA = a1 - a0;
-    if constexpr (Team::size == 64 && MHS_WAVE_PAIRS && F::kPairs) {
+    if constexpr (Team::size == 64 && F::kPairs) {
         wave_walk(a0, a1, Acol, Aval, bmeta, tiles, work, f);
         return;
     }
@@ -2177,7 +2162,6 @@ __device__ __forceinline__ void sym_wave_rows(const SymArgs& a, int bid, int nb)
     const int count = a.stats->sym_count[a.bin];
     const int* list = a.list + (long long)(a.bin - 1) * a.M;
     WaveTeam tm;
-#if MHS_SYM_PREFETCH
     // the wave's next 64 rows and their scalars in one batch (lane j: the row at step j), read
     // back with readlane: the list -> row scalars round trips leave the rows' chains
     const int lane = lane_id();
@@ -2200,10 +2184,6 @@ __device__ __forceinline__ void sym_wave_rows(const SymArgs& a, int bid, int nb)
             sym_row_s(tm, a, r, E, nullptr);
         }
     }
-#else
-    for (RowWalk rw(count, WPB, w, bid, nb); rw.first < rw.end; rw.first += rw.stride)
-        sym_row(tm, a, __builtin_amdgcn_readfirstlane(list[rw.first]), E, nullptr);
-#endif
 }
 
 template <int T, bool GLOBALMEM>
@@ -2763,9 +2743,6 @@ __device__ __forceinline__ int block_row_need(bool b1024, int lo, int hi, int t,
                                                              : (int)num_need(span, t, n, dense_span_max);
 }
 
-#ifndef MHS_SCAN_HOIST
-#define MHS_SCAN_HOIST 0  // 1: k_scan's row scalars load with the counts, before the first barrier (measured slower)
-#endif
 template <int PER>
 __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                unsigned long long* __restrict__ state,
@@ -2781,7 +2758,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                long long* __restrict__ tslot, const int* __restrict__ gna,
                                                int4* __restrict__ bmeta_near) {
     constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
-    static_assert(PER == 1 || PER == 2 || PER == 4, "launch_scan_classify instantiates these");
+    static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
     __shared__ long long excl_s;
     __shared__ int bid_s;
@@ -2831,7 +2808,6 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         v[k] = i < M ? Cptr[i] : 0;
         loc += v[k];
     }
-    if (MHS_SCAN_HOIST) row_scalars();
     {  // total products (off the tail: the last block only publishes)
         const unsigned long long f = wave_sum(fpart);
         if (lane == 0 && f) atomicAdd(&stats->flop, f);
@@ -2850,7 +2826,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                            __HIP_MEMORY_SCOPE_AGENT);
     // numeric bin of every row (independent of the prefix: its loads overlap the
     // predecessors' publication instead of following the look-back)
-    if (!MHS_SCAN_HOIST) row_scalars();
+    row_scalars();  // (loaded here, after the counts' barrier: ahead of it measured slower)
     __shared__ unsigned char nbin_of[ITEMS];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -4000,11 +3976,7 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_common(Sy
 #ifndef MHS_SCAN_BIG_M
 #define MHS_SCAN_BIG_M (1 << 19)
 #endif
-#ifndef MHS_SCAN_PER
-#define MHS_SCAN_PER 4  // k_scan's rows per thread for big M (1, 2 or 4)
-#endif
-static int scan_per(int M) { return M >= MHS_SCAN_BIG_M ? MHS_SCAN_PER : 1; }
-static int bin_list_per(int M) { return M >= MHS_SCAN_BIG_M ? 4 : 1; }
+static int scan_per(int M) { return M >= MHS_SCAN_BIG_M ? 4 : 1; }
 
 #ifndef MHS_ROW_GMIN
 #define MHS_ROW_GMIN 4  // narrowest lane group per row in k_mask_b / k_analyze (tiny rows: 16 per wave)
@@ -4108,7 +4080,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
 void launch_bin_list(const Csr& A, const Work& w, hipStream_t s) {
     const unsigned char* nb = w.nft ? w.nft_bin : nullptr;
     const NearCand nc{w.nsig, (w.groups && !nb) ? w.near_list : nullptr};
-    if (bin_list_per(A.M) == 4)
+    if (scan_per(A.M) == 4)
         hipLaunchKernelGGL(k_bin_list<4>, dim3((A.M + 4095) / 4096), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
                            w.groups, w.bin_list, nb, w.stats, nc);
     else
@@ -4313,7 +4285,6 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
                        w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
                        w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, w.gna, w.near_b ? w.bmeta : nullptr)
     if (per == 4) MHS_SCAN(4);
-    else if (per == 2) MHS_SCAN(2);
     else MHS_SCAN(1);
 #undef MHS_SCAN
 }
