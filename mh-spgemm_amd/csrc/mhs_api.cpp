@@ -354,6 +354,10 @@ constexpr int NUM_GLOBAL_GRID = 128;
 #define MHS_MULTI_FLOP_LOG2 22  // numeric launches over several streams from 2^this products on (round 4: 24 -> 22, scircuit-like numeric -9 %)
 #endif
 
+#ifndef MHS_SPLIT_FLOP_LOG2
+#define MHS_SPLIT_FLOP_LOG2 24  // block bins split by LDS need from 2^this products on
+#endif
+
 // The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
 // the aux streams, which join the call's stream again.
 int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out) {
@@ -374,7 +378,10 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     // one stream the hub rows' launch would no longer overlap the others' bulk).  The partition
     // runs on the call's stream after the fork: only the split launches wait for it (split_ev),
     // the other bins start at once (wb-edu-like: 0.33 ms off the numeric phase's start)
-    const bool split = nss > 1 && ctx->split && launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);
+    // (and only from 2^MHS_SPLIT_FLOP_LOG2 products: on scircuit-like the partition and its event
+    // wait cost more than the split saves -- numeric 0.146 -> 0.119 ms unsplit)
+    const bool split = nss > 1 && ctx->split && h.flop >= (1ull << MHS_SPLIT_FLOP_LOG2) &&
+                       launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);
     if (split) MHS_HIP(hipEventRecord(ctx->split_ev, s));
     const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
                                     ctx->dense_span_max, split, split ? ctx->split_ev : nullptr);

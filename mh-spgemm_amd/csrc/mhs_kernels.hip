@@ -4319,44 +4319,57 @@ int numeric_launches(const Stats& h) {
 struct SplitArgs {
     const int* list[2];
     int count[2], split[2], base[2], on[2];
+    int blk0[3];  // bin k's blocks: [blk0[k], blk0[k+1]) (1024 rows a block)
     int* out;
+    int* ctr;     // per bin: small-row and big-row counters (zeroed with the row cursors)
     const int *rlo, *rhi, *ctiles, *Cptr;
     int dense_span_max;
 };
+constexpr int SPLIT_CURSOR_SLOT = BLOCK_BIG_SLOT + 2;  // k_split_bins' counters (4 of its 8 words)
+static_assert(SPLIT_CURSOR_SLOT < SPILL_CURSOR_SLOT, "split counters below the spill counters");
+// A grid of 1024-row blocks per split bin (one block per bin measured 0.5 ms on wb-edu-like's
+// 56 K block rows, on the block launches' critical path): LDS offsets within the block, then one
+// counter add per block and kind.  Order within the small and the big rows is by block arrival
+// (the block launches take their rows from a queue anyway).
 __global__ __launch_bounds__(1024) void k_split_bins(SplitArgs a) {
-    const int k = blockIdx.x;
-    if (!a.on[k]) return;
-    __shared__ int nsmall, nbig;
+    const int k = (int)blockIdx.x < a.blk0[1] ? 0 : 1;
+    const int i = ((int)blockIdx.x - a.blk0[k]) * 1024 + (int)threadIdx.x;
+    __shared__ int nsmall, nbig, gsmall, gbig;
     if (threadIdx.x == 0) nsmall = nbig = 0;
     __syncthreads();
     const int count = a.count[k], lane = lane_id();
+    int row = 0;
+    bool big = false;
+    if (i < count) {
+        row = a.list[k][i];
+        big = block_row_need(k == 1, a.rlo[row], a.rhi[row], a.ctiles[row], a.Cptr[row + 1] - a.Cptr[row],
+                             a.dense_span_max) > a.split[k];
+    }
+    const unsigned long long bb = __ballot(i < count && big), bs = __ballot(i < count && !big);
+    int ob = 0, os = 0;
+    if (lane == 0) {
+        if (bb) ob = atomicAdd(&nbig, __popcll(bb));
+        if (bs) os = atomicAdd(&nsmall, __popcll(bs));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int* c = a.ctr + k * 2 * CURSOR_STRIDE;
+        gsmall = nsmall ? atomicAdd(c, nsmall) : 0;
+        gbig = nbig ? atomicAdd(c + CURSOR_STRIDE, nbig) : 0;
+    }
+    __syncthreads();
+    ob = __shfl(ob, 0) + gbig;
+    os = __shfl(os, 0) + gsmall;
     int* out = a.out + a.base[k];
-    for (int i0 = threadIdx.x & ~63; i0 < count; i0 += 1024) {
-        const int i = i0 + lane;
-        int row = 0;
-        bool big = false;
-        if (i < count) {
-            row = a.list[k][i];
-            big = block_row_need(k == 1, a.rlo[row], a.rhi[row], a.ctiles[row], a.Cptr[row + 1] - a.Cptr[row],
-                                 a.dense_span_max) > a.split[k];
-        }
-        const unsigned long long bb = __ballot(i < count && big), bs = __ballot(i < count && !big);
-        int ob = 0, os = 0;
-        if (lane == 0) {
-            if (bb) ob = atomicAdd(&nbig, __popcll(bb));
-            if (bs) os = atomicAdd(&nsmall, __popcll(bs));
-        }
-        ob = __shfl(ob, 0);
-        os = __shfl(os, 0);
-        if (i < count) {
-            if (big) out[count - 1 - (ob + __popcll(bb & lanemask_lt()))] = row;
-            else out[os + __popcll(bs & lanemask_lt())] = row;
-        }
+    if (i < count) {
+        if (big) out[count - 1 - (ob + __popcll(bb & lanemask_lt()))] = row;
+        else out[os + __popcll(bs & lanemask_lt())] = row;
     }
 }
 
 bool launch_split_bins(const Work& w, const Stats& h, int M, const int* Cptr, hipStream_t s, int dense_span_max) {
     SplitArgs a{};
+    // bin 0 of the kernel is NUM_B256 (its list after NUM_B1024's in split_list), bin 1 NUM_B1024
     const int bins[2] = {NUM_B256, NUM_B1024};
     const int splits[2] = {B256_SPLIT, B1024_SPLIT};
     for (int k = 0; k < 2; ++k) {
@@ -4364,17 +4377,19 @@ bool launch_split_bins(const Work& w, const Stats& h, int M, const int* Cptr, hi
         a.count[k] = h.num_count[bins[k]] > 0 ? h.num_count[bins[k]] : 0;
         a.split[k] = splits[k];
         a.on[k] = block_split_on(h, k);
+        a.blk0[k + 1] = a.blk0[k] + (a.on[k] ? (a.count[k] + 1023) / 1024 : 0);
     }
     if (!a.on[0] && !a.on[1]) return false;
     a.base[1] = 0;
     a.base[0] = a.count[1];
     a.out = w.split_list;
+    a.ctr = w.cursors + SPLIT_CURSOR_SLOT * 8 * CURSOR_STRIDE;
     a.rlo = w.rlo;
     a.rhi = w.rhi;
     a.ctiles = w.ctiles;
     a.Cptr = Cptr;
     a.dense_span_max = dense_span_max;
-    hipLaunchKernelGGL(k_split_bins, dim3(2), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_split_bins, dim3(a.blk0[2]), dim3(1024), 0, s, a);
     return true;
 }
 
