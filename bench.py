@@ -15,8 +15,8 @@ partitioned by flop, each rank starts with its row block of A (= of B); the
 exchange plan is built once (mhspgemm.distributed.ShardPlan, outside the timed
 steps) and a step is the exchange of B's rows over xGMI (--exchange halo: the
 rows the block references; full: the north_star's allgatherv of every block)
-+ the local SpGEMM; C stays distributed (--gather times the gatherv to rank 0
-beside it).  Total work is fixed, so scaling is "strong".
++ the local SpGEMM; C stays distributed in `value`, and the gatherv of C to rank 0
+is timed beside it (gather_C_ms, value_C_gathered; --no-gather skips it).  Total work is fixed, so scaling is "strong".
 
 One JSON line on rank 0: value = 2*flop / (max over ranks of the time per step).
   roofline: the dominant kernel = the numeric phase (every numeric bin launch of a
@@ -155,7 +155,9 @@ def main():
     ap.add_argument("--matrix", default=None,
                     help="default: cant (BASELINE configs[1]) on 1 GPU, cage15 (configs[4], row-sharded) on N > 1")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--gather", action="store_true", help="N>1: also time the gatherv of C to rank 0")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: skip timing the gatherv of C to rank 0 (timed by default: SURVEY §8(e) asks for "
+                         "the speed-up with C distributed and with C gathered)")
     ap.add_argument("--exchange", default="full", choices=["halo", "full"],
                     help="N>1: B rows moved per step: every row block (full: the north_star's allgatherv, "
                          "the headline) or only the referenced rows (halo); the other mode is timed beside it")
@@ -278,7 +280,7 @@ def main():
                 fm = mhspgemm.flop_count_np(Am.col, Am.ptr)
                 Am.H2D(local)
                 st = max(3, min(args.steps, 10 if Am.M > 1_000_000 else args.steps))
-                el, nms = time_steps(Am, st, min(args.warmup, 3))
+                el, nms = time_steps(Am, st, max(1, min(args.warmup, 3)))  # >= 1: workspace growth untimed
                 C, tm = mhspgemm.spgemm(tool, Am, Am, timing=True)
                 C.release()
                 ms = el / st * 1e3
@@ -290,6 +292,7 @@ def main():
                     "numeric_ms": round(avg_n, 4), "compulsory_bytes": bcm,
                     "frac_numeric": round(bcm / (avg_n * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                     "frac_e2e": round(bcm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                    "_frac_e2e": bcm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                     "phases_ms": {k: round(getattr(tm, k), 4) for k in (
                         "Form_mask_matrix_B", "symbolic_binning", "Calculate_C_nnz", "numeric_binning", "Numeric",
                         "total_e2e")},
@@ -341,7 +344,7 @@ def main():
         del s_col, s_val
         barrier()
         p0 = time.perf_counter()
-        blk = D.rebalance(eq, M_glob)
+        blk = D.rebalance(eq, M_glob, compute=dev)  # (rehearsal: host block, GPU gathers)
         del eq
         plan = D.ShardPlan(blk, M_glob, mode=args.exchange)
         barrier()
@@ -380,15 +383,26 @@ def main():
         alt_plan = D.ShardPlan(blk, M_glob, mode=alt_mode)
         t_alt, (_, alt_bytes, _) = timed(alt_plan)
         del alt_plan
-        if args.gather:
+        if not args.no_gather:
+            # gatherv of C's row blocks to rank 0 (the speed-up is reported with C
+            # distributed and with C gathered); median of 3, max over ranks
             tool.set_option(L.MHS_OPT_SYNC, 1)
             C, _ = D.spgemm_planned(plan, mult)
-            barrier()
-            g0 = time.perf_counter()
-            D.gather_result(C if xdev == dev else tuple(x.cpu() for x in C.to_torch()), blk)
-            barrier()
-            gather_ms = (time.perf_counter() - g0) * 1e3
+            Cs = C if xdev == dev else tuple(x.cpu() for x in C.to_torch())
+            gt = []
+            for _ in range(3):
+                barrier()
+                g0 = time.perf_counter()
+                g = D.gather_result(Cs, blk)
+                barrier()
+                gt.append((time.perf_counter() - g0) * 1e3)
+                del g
+            tt = torch.tensor([float(np.median(gt))], dtype=torch.float64, device=xdev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            gather_ms = float(tt.item())
+            del Cs
             C.release()
+            log(f"gatherv(C) to rank 0: {gather_ms:.3f} ms")
 
     ms_per_step = t_max / args.steps * 1e3
     gflops = 2.0 * flop / (ms_per_step * 1e-3) / 1e9
@@ -450,8 +464,9 @@ def main():
         out["hbm_peak"] = dict(hbm, spec_GBps=HBM_PEAK_GBPS,
                                kernels="mhs_hbm_peak: 16 B a lane, 4 in flight, 16 blocks per CU, 2 GiB buffers, cached or nontemporal stores (the better)")
         if configs:
-            geo = float(np.exp(np.mean([np.log(c["frac_e2e"]) for c in configs + [
-                {"frac_e2e": b_comp(M_glob, nnzA, nnzC) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}]])))
+            fr = [c.pop("_frac_e2e") for c in configs]  # unrounded
+            fr.append(b_comp(M_glob, nnzA, nnzC) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS)
+            geo = float(np.exp(np.mean(np.log(fr))))
             out["configs"] = {"matrices": configs, "geomean_frac_e2e_with_headline": round(geo, 4),
                               "note": "same pipelined steps as value; frac_* = compulsory bytes "
                                       "8(M+1) + 12 nnz(A) + 12 nnz(C) over the numeric phase / the whole step, "
@@ -490,10 +505,12 @@ def main():
         ms_alt = t_alt / args.steps * 1e3
         out["exchange_alt"] = {"mode": alt_mode, "value": round(2.0 * flop / (ms_alt * 1e-3) / 1e9, 2),
                                "ms_per_step": round(ms_alt, 4), "bytes_in_per_step_all_ranks": alt_bytes}
-        if gather_ms is not None:
-            out["gather_C_ms"] = round(gather_ms, 3)
         out["single_gpu_same_matrix"] = one_gpu
         out["speedup_vs_1gpu"] = round(one_gpu["ms_per_step"] / ms_per_step, 3)
+        if gather_ms is not None:
+            out["gather_C_ms"] = round(gather_ms, 3)
+            out["speedup_vs_1gpu_C_gathered"] = round(one_gpu["ms_per_step"] / (ms_per_step + gather_ms), 3)
+            out["value_C_gathered"] = round(2.0 * flop / ((ms_per_step + gather_ms) * 1e-3) / 1e9, 2)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

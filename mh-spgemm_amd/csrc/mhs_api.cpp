@@ -1026,4 +1026,13 @@ int mhs_device_free(mhs_ctx* ctx, void* p) {
     return MHS_OK;
 }
 
+int mhs_hbm_peak(mhs_ctx* ctx, size_t bytes, int iters, double* gbps) {
+    if (!ctx) return MHS_ERR_INVALID;
+    if (!gbps || iters <= 0 || bytes < (1u << 20))
+        return fail(ctx, MHS_ERR_INVALID, "mhs_hbm_peak: needs gbps[3], iters > 0 and bytes >= 1 MiB");
+    MHS_HIP(hipSetDevice(ctx->device));
+    MHS_HIP(hbm_peak_run(bytes, iters, gbps));
+    return MHS_OK;
+}
+
 }  // extern "C"

@@ -440,5 +440,7 @@ hipError_t transpose_csr(const Csr& A, int* tptr, int* tcol, double* tval, void*
 hipError_t init_kernel_attributes();
 // device address of the probe-conflict counter (nullptr unless built with MHS_PROBE_STATS=1)
 hipError_t probe_counter(unsigned long long** dev);
+// mhs_hbm.hip: the streaming kernels of mhs_hbm_peak on the current device (gbps[3]: copy, read, write)
+hipError_t hbm_peak_run(size_t bytes, int iters, double* gbps);
 
 }  // namespace mhs

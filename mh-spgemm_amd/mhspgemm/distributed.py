@@ -87,13 +87,15 @@ def equal_rows(M: int, P: int, p: int):
     return (M * p) // P, (M * (p + 1)) // P
 
 
-def rebalance(blk: Block, M_global: int, group=None) -> Block:
+def rebalance(blk: Block, M_global: int, group=None, compute=None) -> Block:
     """Distributed flop-balanced partition: from any contiguous row blocks (e.g. the
     equal-row blocks each rank read), compute the cuts of `partition_rows` over the
     global per-row flop without any rank holding the whole matrix, then move rows to
     their new owners.  Traffic: the global row lengths (4 B per row, all-gathered: the
     flop of a row needs the lengths of the B rows it names) plus the rows that change
-    owner.  Returns this rank's new block (same contents as `local_block` of the cuts)."""
+    owner.  Returns this rank's new block (same contents as `local_block` of the cuts).
+    `compute`: device of the per-row flop gathers when the block lives elsewhere (a gloo
+    rehearsal keeps the block on the host but computes on the GPU)."""
     import torch
     import torch.distributed as dist
     P = dist.get_world_size(group)
@@ -108,10 +110,13 @@ def rebalance(blk: Block, M_global: int, group=None) -> Block:
     _p2p_allgatherv(lens, glen, roff, rows, group)
     # 2. local per-row flop, inclusive prefix, per-rank totals
     nloc = blk.r1 - blk.r0
-    per = glen.index_select(0, blk.col.long()).to(torch.int64)
-    rid = torch.repeat_interleave(torch.arange(nloc, device=dev), lens.long())
-    f = torch.zeros(nloc, dtype=torch.int64, device=dev).index_add_(0, rid, per)
-    pre = torch.cumsum(f, 0)
+    # (row sums as differences of one prefix over the entries: no per-entry row ids)
+    cdev = compute if compute is not None else dev
+    per = glen.to(cdev).index_select(0, blk.col.to(cdev).long()).to(torch.int64)
+    cs = torch.zeros(per.numel() + 1, dtype=torch.int64, device=cdev)
+    torch.cumsum(per, 0, out=cs[1:])
+    pre = (cs.index_select(0, blk.ptr[1:].to(cdev).long()) - cs[int(blk.ptr[0])]).to(dev)
+    del per, cs
     tot = torch.tensor([int(pre[-1]) if nloc else 0], dtype=torch.int64, device=dev)
     tots = torch.zeros(P, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(tots, tot, group=group)
@@ -325,7 +330,14 @@ class ShardPlan:
     columns reference; "full": every row (the north_star's allgatherv).  The
     local B keeps rows in ascending global order (owners' ranges are ascending
     and each request list is sorted), so consecutive rows stay consecutive (FEM
-    dof runs) and A's renumbered columns stay sorted per row."""
+    dof runs) and A's renumbered columns stay sorted per row.
+
+    Round 5: the plan is built with torch ops on the block's device (the GPU under
+    RCCL) instead of host numpy -- the round-4 build took 4.9 s at N = 2 on
+    cage15-like, most of it np.searchsorted / np.repeat over the block's 50 M
+    columns -- and the full mode needs no index lists at all: every peer receives
+    the sender's whole block, so a step sends the block's own arrays and A's
+    columns are already local B ids."""
 
     def __init__(self, blk: Block, M_global: int, group=None, mode: str = "halo"):
         import torch
@@ -337,62 +349,64 @@ class ShardPlan:
         self.P, self.me = P, me
         dev = blk.col.device
         self.dev = dev
-        # 1. row ranges of every rank
-        rr = torch.tensor([blk.r0, blk.r1], dtype=torch.int64, device=dev)
-        allr = torch.zeros(2 * P, dtype=torch.int64, device=dev)
+        # 1. row ranges and nnz of every rank
+        rr = torch.tensor([blk.r0, blk.r1, blk.col.numel()], dtype=torch.int64, device=dev)
+        allr = torch.zeros(3 * P, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(allr, rr, group=group)
-        rng = allr.cpu().numpy().reshape(P, 2)
-        self.ranges = rng
-        lptr = blk.ptr.cpu().numpy().astype(np.int64)
-        lcol = blk.col.cpu().numpy()
-        # 2. rows this rank needs from every owner (sorted, global ids)
-        if mode == "full":
-            need = [np.arange(rng[q, 0], rng[q, 1], dtype=np.int64) for q in range(P)]
-        else:
-            u = np.unique(lcol.astype(np.int64))
-            need = [u[(u >= rng[q, 0]) & (u < rng[q, 1])] for q in range(P)]
-        cnt = torch.tensor([len(x) for x in need], dtype=torch.int64, device=dev)
-        cnt_in = torch.zeros(P, dtype=torch.int64, device=dev)
-        dist.all_to_all_single(cnt_in, cnt, group=group)
-        cnt_in = cnt_in.cpu().numpy()
-        req = torch.from_numpy(np.concatenate(need) if P else np.zeros(0, np.int64)).to(dev)
-        req_in = torch.zeros(int(cnt_in.sum()), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(req_in, req, output_split_sizes=cnt_in.tolist(), input_split_sizes=cnt.cpu().tolist(),
-                               group=group)
-        req_in = req_in.cpu().numpy()
-        # 3. what this rank sends: rows (local ids) and their entries, per peer
-        send_rows, send_elems, send_nnz = [], [], []
-        off = 0
-        for q in range(P):
-            rows = req_in[off:off + cnt_in[q]] - blk.r0
-            off += cnt_in[q]
-            send_rows.append(rows)
-            lens = lptr[rows + 1] - lptr[rows]
-            send_nnz.append(int(lens.sum()))
-            send_elems.append(np.repeat(lptr[rows], lens) + (np.arange(lens.sum()) - np.repeat(np.cumsum(lens) - lens, lens)))
-        nnz_out = torch.tensor(send_nnz, dtype=torch.int64, device=dev)
-        nnz_in = torch.zeros(P, dtype=torch.int64, device=dev)
-        dist.all_to_all_single(nnz_in, nnz_out, group=group)
-        nnz_in = nnz_in.cpu().numpy()
-        self.srows = [len(x) for x in send_rows]
-        self.snnz = send_nnz
-        self.rrows = [len(x) for x in need]
-        self.rnnz = [int(x) for x in nnz_in]
-        self.soff_r = np.concatenate([[0], np.cumsum(self.srows)])
-        self.soff_n = np.concatenate([[0], np.cumsum(self.snnz)])
-        self.roff_r = np.concatenate([[0], np.cumsum(self.rrows)])
-        self.roff_n = np.concatenate([[0], np.cumsum(self.rnnz)])
-        cat = lambda xs: np.concatenate(xs) if len(xs) else np.zeros(0, np.int64)  # noqa: E731
-        self.sidx_rows = torch.from_numpy(cat(send_rows).astype(np.int64)).to(dev)
-        self.sidx_elems = torch.from_numpy(cat(send_elems).astype(np.int64)).to(dev)
+        rng = allr.cpu().numpy().reshape(P, 3)
+        self.ranges = rng[:, :2]
         self.rowlen = (blk.ptr[1:] - blk.ptr[:-1]).to(torch.int32)
-        # 4. local B rows (ascending global ids) and A's columns renumbered into them
-        self.brows = cat(need).astype(np.int64)
-        self.nB = len(self.brows)
+        nrow, nnz = blk.r1 - blk.r0, blk.col.numel()
+        if mode == "full":
+            # every peer gets this rank's whole block; this rank gets every block
+            self.srows = [nrow] * P
+            self.snnz = [nnz] * P
+            self.rrows = [int(rng[q, 1] - rng[q, 0]) for q in range(P)]
+            self.rnnz = [int(rng[q, 2]) for q in range(P)]
+            self.sidx_rows = self.sidx_elems = None
+            self.acol_local = blk.col  # B holds every row in order: global ids are local ids
+            self._brows_t = None
+        else:
+            # 2. rows this rank needs from every owner (sorted, global ids), split by owner
+            u = torch.unique(blk.col.to(torch.int64))  # sorted
+            starts = torch.from_numpy(np.ascontiguousarray(rng[:, 0])).to(dev)
+            cut = torch.searchsorted(u, starts).cpu().numpy().tolist() + [u.numel()]
+            cnt = [cut[q + 1] - cut[q] for q in range(P)]
+            cnt_t = torch.tensor(cnt, dtype=torch.int64, device=dev)
+            cnt_in_t = torch.zeros(P, dtype=torch.int64, device=dev)
+            dist.all_to_all_single(cnt_in_t, cnt_t, group=group)
+            cnt_in = cnt_in_t.cpu().numpy().tolist()
+            req_in = torch.zeros(int(sum(cnt_in)), dtype=torch.int64, device=dev)
+            dist.all_to_all_single(req_in, u, output_split_sizes=cnt_in, input_split_sizes=cnt, group=group)
+            # 3. what this rank sends: rows (local ids) and their entries, per peer
+            rows = req_in - blk.r0
+            lens = self.rowlen.index_select(0, rows).to(torch.int64)
+            rb = blk.ptr.index_select(0, rows).to(torch.int64)
+            tot = int(lens.sum()) if lens.numel() else 0
+            first = torch.cumsum(lens, 0) - lens
+            self.sidx_elems = (torch.repeat_interleave(rb - first, lens) +
+                               torch.arange(tot, dtype=torch.int64, device=dev))
+            self.sidx_rows = rows
+            seg = np.concatenate([[0], np.cumsum(cnt_in)]).astype(np.int64)
+            cl = torch.cumsum(lens, 0).cpu().numpy() if lens.numel() else np.zeros(0, np.int64)
+            ends = [int(cl[seg[q + 1] - 1]) if seg[q + 1] > 0 else 0 for q in range(P)]
+            send_nnz = [ends[q] - (ends[q - 1] if q else 0) for q in range(P)]
+            nnz_out = torch.tensor(send_nnz, dtype=torch.int64, device=dev)
+            nnz_in = torch.zeros(P, dtype=torch.int64, device=dev)
+            dist.all_to_all_single(nnz_in, nnz_out, group=group)
+            self.srows = cnt_in
+            self.snnz = send_nnz
+            self.rrows = cnt
+            self.rnnz = [int(x) for x in nnz_in.cpu().numpy()]
+            # 4. local B rows = u (ascending global ids); A's columns renumbered into them
+            self._brows_t = u
+            self.acol_local = torch.searchsorted(u, blk.col.to(torch.int64)).to(torch.int32)
+        self.soff_r = np.concatenate([[0], np.cumsum(self.srows)]).astype(np.int64)
+        self.soff_n = np.concatenate([[0], np.cumsum(self.snnz)]).astype(np.int64)
+        self.roff_r = np.concatenate([[0], np.cumsum(self.rrows)]).astype(np.int64)
+        self.roff_n = np.concatenate([[0], np.cumsum(self.rnnz)]).astype(np.int64)
+        self.nB = int(self.roff_r[-1])
         self.Bnnz = int(self.roff_n[-1])
-        pos = np.searchsorted(self.brows, lcol.astype(np.int64))
-        assert len(lcol) == 0 or np.array_equal(self.brows[np.minimum(pos, self.nB - 1)], lcol), "column not planned"
-        self.acol_local = torch.from_numpy(pos.astype(np.int32)).to(dev)
         self.M_global = M_global
         # receive buffers (reused every step)
         self.Blen = torch.empty(self.nB, dtype=torch.int32, device=dev)
@@ -401,32 +415,51 @@ class ShardPlan:
         self.Bptr = torch.zeros(self.nB + 1, dtype=torch.int32, device=dev)
         self.bytes_in = 4 * self.nB + 12 * self.Bnnz - (4 * self.rrows[me] + 12 * self.rnnz[me])
 
+    @property
+    def brows(self) -> np.ndarray:
+        """Global ids of the local B rows (ascending)."""
+        if self._brows_t is None:
+            return np.arange(self.M_global, dtype=np.int64)
+        return self._brows_t.cpu().numpy()
+
+    def _packed(self):
+        """(row lengths, columns, values) to send, concatenated over peers in rank order
+        (full mode: the block itself, the same slice for every peer)."""
+        blk = self.blk
+        if self.sidx_rows is None:
+            return self.rowlen, blk.col, blk.val
+        return (self.rowlen.index_select(0, self.sidx_rows), blk.col.index_select(0, self.sidx_elems),
+                blk.val.index_select(0, self.sidx_elems))
+
     def exchange(self):
         """One step: pack the requested rows, P2P them into place, rebuild B's row
         pointer.  Returns (Bptr, Bcol, Bval) over the local B rows."""
         import torch
         import torch.distributed as dist
-        blk, me, P = self.blk, self.me, self.P
-        sl = self.rowlen.index_select(0, self.sidx_rows)
-        sc = blk.col.index_select(0, self.sidx_elems)
-        sv = blk.val.index_select(0, self.sidx_elems)
+        me, P = self.me, self.P
+        full = self.sidx_rows is None
+        sl, sc, sv = self._packed()
+
+        def out_slice(q):  # this rank's send slice for peer q
+            if full:
+                return (0, self.srows[q]), (0, self.snnz[q])
+            return (self.soff_r[q], self.soff_r[q + 1]), (self.soff_n[q], self.soff_n[q + 1])
+
+        (s0, s1), (e0, e1) = out_slice(me)
         r0, r1 = self.roff_r[me], self.roff_r[me + 1]
         n0, n1 = self.roff_n[me], self.roff_n[me + 1]
-        s0, s1 = self.soff_r[me], self.soff_r[me + 1]
-        e0, e1 = self.soff_n[me], self.soff_n[me + 1]
         self.Blen[r0:r1].copy_(sl[s0:s1])
         self.Bcol[n0:n1].copy_(sc[e0:e1])
         self.Bval[n0:n1].copy_(sv[e0:e1])
         ops = []
         for k in range(1, P):  # ring order spreads the pairs over the xGMI links
             dst, src = (me + k) % P, (me - k) % P
+            (a, b), (c, d) = out_slice(dst)
             if self.srows[dst]:
-                a, b = self.soff_r[dst], self.soff_r[dst + 1]
                 ops.append(dist.P2POp(dist.isend, sl[a:b], dst, self.group))
             if self.snnz[dst]:
-                a, b = self.soff_n[dst], self.soff_n[dst + 1]
-                ops.append(dist.P2POp(dist.isend, sc[a:b], dst, self.group))
-                ops.append(dist.P2POp(dist.isend, sv[a:b], dst, self.group))
+                ops.append(dist.P2POp(dist.isend, sc[c:d], dst, self.group))
+                ops.append(dist.P2POp(dist.isend, sv[c:d], dst, self.group))
             if self.rrows[src]:
                 ops.append(dist.P2POp(dist.irecv, self.Blen[self.roff_r[src]:self.roff_r[src + 1]], src, self.group))
             if self.rnnz[src]:
