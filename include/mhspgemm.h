@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 8
+#define MHS_ABI_VERSION 9
 
 typedef enum mhs_status {
     MHS_OK = 0,
@@ -111,6 +111,17 @@ typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2, MHS_OPT_
 int mhs_ctx_set_option(mhs_ctx *ctx, int option, int value);
 /* Calls of this context that ran row-chunked (the out-of-memory fallback). */
 long long mhs_ctx_chunked_calls(const mhs_ctx *ctx);
+/* Path counters of this context (diagnostics, ABI v9): calls that ran
+ *   MHS_STAT_CHUNKED      row-chunked (as mhs_ctx_chunked_calls),
+ *   MHS_STAT_SPLIT        their numeric block bins split by LDS need (k_split_bins),
+ *   MHS_STAT_SYM_FORK     the rare symbolic bins on an aux stream beside the common ones,
+ *   MHS_STAT_NFT          numeric-first tiny rows (value slots filled by the symbolic pass),
+ *   MHS_STAT_NEAR         near row groups verified (union rows built),
+ *   MHS_STAT_MULTI_STREAM numeric launches dealt over several streams.
+ * Returns -1 for a null context or an unknown counter. */
+typedef enum mhs_stat { MHS_STAT_CHUNKED = 0, MHS_STAT_SPLIT = 1, MHS_STAT_SYM_FORK = 2, MHS_STAT_NFT = 3,
+                        MHS_STAT_NEAR = 4, MHS_STAT_MULTI_STREAM = 5 } mhs_stat;
+long long mhs_ctx_stat(const mhs_ctx *ctx, int which);
 /* Numeric-phase durations (ms) of the last min(n, recorded) calls, oldest
  * first; waits for them.  Returns the count written, or -status on error. */
 int mhs_ctx_numeric_ms(mhs_ctx *ctx, float *out, int n);

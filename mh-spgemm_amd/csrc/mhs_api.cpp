@@ -59,12 +59,17 @@ struct mhs_ctx {
     long long sym_fork_min_m = 1 << 19;
     bool nft_slots = true;   // MHS_NFT_NO_SLOTS=1 (tests): count the rows only, as when the slots do not fit
     int nft_other_pct = 5;   // slots only when at most this share of the rows is past the tiny classes (MHS_NFT_OTHER_PCT)
+    // numeric-first tiny rows without the probe below nft_min_m rows, for matrices averaging fewer
+    // than this many entries a row (MHS_NFT_AUTO_AVG; 0: off): the slots are sized by their upper
+    // bound (TINY_SLOT_MAX a row), so no hand-off decides them
+    int nft_auto_avg = 12;
     char* slots = nullptr;   // their value slots (cached across calls)
     size_t slots_bytes = 0;
     size_t mem_budget = 0;   // MHS_OPT_MEM_BUDGET (MiB): a call's workspace + C beyond it count as OOM (tests)
     size_t c_held = 0;       // C bytes a row-chunked call holds while it lays out its second pass
     long long front_passes = 0;  // front_pass calls (row-chunked passes; mhs_ctx_chunked_calls diagnostics)
     long long chunked_calls = 0;  // calls that ran row-chunked (mhs_ctx_chunked_calls)
+    long long stat[6] = {};       // path counters (mhs_ctx_stat; [0] unused: chunked_calls)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays): (buffer, allocation size)
     std::vector<std::pair<void*, size_t>> pool;
@@ -383,6 +388,8 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     const bool split = nss > 1 && ctx->split && h.flop >= (1ull << MHS_SPLIT_FLOP_LOG2) &&
                        launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);
     if (split) MHS_HIP(hipEventRecord(ctx->split_ev, s));
+    ctx->stat[MHS_STAT_SPLIT] += split;
+    ctx->stat[MHS_STAT_MULTI_STREAM] += nss > 1;
     const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
                                     ctx->dense_span_max, split, split ? ctx->split_ev : nullptr);
     MHS_HIP(hipGetLastError());
@@ -600,6 +607,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_SYM_FORK")) ctx->sym_fork = atoi(e) != 0;
     if (const char* e = getenv("MHS_SYM_FORK_MIN_M")) ctx->sym_fork_min_m = atoll(e);
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
+    if (const char* e = getenv("MHS_NFT_AUTO_AVG")) ctx->nft_auto_avg = atoi(e);
     *out = ctx;
     return MHS_OK;
 }
@@ -704,9 +712,13 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // ---- mem_alloc: workspace (cached across calls) + C.ptr --------------------
     const int mc_list = ctx->mc_list > 0 ? ctx->mc_list : mc_list_for(M);
     const bool probe = ctx->tiny_num && ctx->nft_min_m >= 0 && M >= ctx->nft_min_m && M > 0;
+    // numeric-first without the probe (short-row matrices below nft_min_m rows): every tiny row
+    // is sorted once, in symbolic, into slots sized by the per-row bound
+    const bool nft_auto = !probe && M > 0 && ctx->tiny_num && ctx->nft_slots && ctx->nft_auto_avg > 0 &&
+                          A->nnz < (long long)ctx->nft_auto_avg * M;
     // near row groups: with the row cache (their C patterns are compared there), not with
     // the numeric-first probe (big M), and union rows of at most 3 x 32 M values
-    bool near = ctx->near && ctx->groups && ctx->use_mcache && !probe && A->nnz <= (1 << 25);
+    bool near = ctx->near && ctx->groups && ctx->use_mcache && !probe && !nft_auto && A->nnz <= (1 << 25);
     const bool same_ab = A->ptr == B->ptr && A->col == B->col && A->val == B->val;
     Layout L = plan(M, MB, A->nnz, B->nnz, mc_list, -1, near, near && same_ab);
     const char* ws_before = ctx->ws;
@@ -754,8 +766,19 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // them; the host picks the bin lists and sizes the candidates' value slots
     unsigned long long other = 0;
     if (probe) w.nft_bin = (unsigned char*)(ctx->ws + L.nft_bin);
+    if (nft_auto) {
+        const size_t n = (size_t)M * TINY_SLOT_MAX;
+        if (ensure(ctx, &ctx->slots, &ctx->slots_bytes, n * 12) == MHS_OK) {
+            w.nft_bin = (unsigned char*)(ctx->ws + L.nft_bin);
+            w.nft = 1;
+            w.sc_val = (double*)ctx->slots;
+            w.sc_col = (int*)(ctx->slots + n * 8);
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     const int seq_probe = probe ? ++ctx->seq : 0;
-    launch_analyze(a, w, MB, s, out.ptr, ctx->d_pub, seq_probe);
+    launch_analyze(a, w, MB, s, out.ptr, probe ? ctx->d_pub : nullptr, seq_probe);
     if (probe) {
         MHS_HIP(hipGetLastError());
         rc = wait_published(ctx, s, ctx->pub, seq_probe);
@@ -785,6 +808,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // common bins -- their tail no longer idles the chip
     const bool fork_big = ctx->sym_fork_min_m >= 0 && M >= ctx->sym_fork_min_m;
     if (((w.nft && other > 0) || ctx->sym_fork || fork_big) && ctx->num_streams > 1 && ctx->aux[0]) {
+        ++ctx->stat[MHS_STAT_SYM_FORK];
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
         launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0], false);
@@ -833,6 +857,8 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         return fail(ctx, (h.err & ERR_OVERFLOW) ? MHS_ERR_OVERFLOW : MHS_ERR_INVALID, m);
     }
     out.nnz = (int)h.nnzC;
+    ctx->stat[MHS_STAT_NFT] += w.nft != 0;
+    ctx->stat[MHS_STAT_NEAR] += L.near && h.near_verified > 0;
 
     // ---- Malloc_C_col_val ---------------------------------------------------------------
     const auto T5 = std::chrono::steady_clock::now();
@@ -971,6 +997,11 @@ int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
 }
 
 long long mhs_ctx_chunked_calls(const mhs_ctx* ctx) { return ctx ? ctx->chunked_calls : -1; }
+
+long long mhs_ctx_stat(const mhs_ctx* ctx, int which) {
+    if (!ctx || which < 0 || which > MHS_STAT_MULTI_STREAM) return -1;
+    return which == MHS_STAT_CHUNKED ? ctx->chunked_calls : ctx->stat[which];
+}
 
 int mhs_ctx_numeric_ms(mhs_ctx* ctx, float* out, int n) {
     if (!ctx || (!out && n > 0)) return -MHS_ERR_INVALID;

@@ -15,6 +15,9 @@
 // (entry point mhs_hbm_peak in mhs_api.cpp).
 #include "mhs_internal.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace mhs {
 namespace {
 
@@ -111,9 +114,11 @@ void l_write(int g, hipStream_t s, v4i*, v4i* b, long long n, int*) {
 const Shape kShapes[] = {
     {0, 16, l_copy<true, 4, false>},  {0, 16, l_copy<false, 4, false>}, {0, 8, l_copy<true, 8, false>},
     {0, 8, l_copy<false, 8, false>},  {0, 4, l_copy<true, 8, true>},    {0, 8, l_copy<true, 8, true>},
-    {0, 8, l_copy<false, 8, true>},   {0, 16, l_copy<true, 4, true>},   {1, 16, l_read<4, false>},
-    {1, 8, l_read<8, false>},         {1, 8, l_read<8, true>},          {2, 16, l_write<true>},
-    {2, 16, l_write<false>},
+    {0, 8, l_copy<false, 8, true>},   {0, 16, l_copy<true, 4, true>},   {0, 4, l_copy<true, 16, false>},
+    {0, 2, l_copy<true, 16, true>},   {0, 32, l_copy<true, 2, false>},  {0, 32, l_copy<false, 2, false>},
+    {1, 16, l_read<4, false>},        {1, 8, l_read<8, false>},         {1, 8, l_read<8, true>},
+    {2, 16, l_write<true>},           {2, 16, l_write<false>},          {2, 4, l_write<true>},
+    {2, 32, l_write<false>},
 };
 
 }  // namespace
@@ -154,6 +159,9 @@ hipError_t hbm_peak_run(size_t bytes, int iters, double* gbps) {
         const double moved = (double)bytes * (sh.kind == 0 ? 2.0 : 1.0) * iters;
         const double r = e == hipSuccess && ms > 0.f ? moved / (ms * 1e-3) / 1e9 : 0.0;
         if (r > best[sh.kind]) best[sh.kind] = r;
+        if (getenv("MHS_HBM_VERBOSE"))
+            fprintf(stderr, "hbm shape %d (kind %d, %d blocks/CU): %.1f GB/s\n", (int)(&sh - kShapes), sh.kind,
+                    sh.per_cu, r);
     }
     for (int k = 0; k < 3; ++k) gbps[k] = best[k];
     if (s) (void)hipStreamSynchronize(s);

@@ -63,6 +63,7 @@ __host__ __device__ constexpr int tiny_k(int c) { return c == 0 ? 2 : c == 5 ? 8
 __host__ __device__ constexpr int tiny_ws(int c) { return c <= 2 ? 8 : 32; }
 __host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? 1 : c == 2 ? 8 : 4; }
 constexpr int TINY_FUSED_KMAX = 4;  // largest K of the numeric classes 0..3 (one fused launch)
+constexpr int TINY_SLOT_MAX = 128;  // value slots of a numeric-first row: W*K of its class (0..3), at most 32*4
 // Symbolic uses the classes below TINY_SYM_NC only (past 128 products a hash table
 // counts faster than a sort); numeric uses the 64-lane classes for rows whose table
 // would not fit the small wave bin (measured: cop20k-like 2.3x slower sorted, while
@@ -285,6 +286,7 @@ __host__ __device__ inline int num_mode(int span, int t, int n, int dense_span_m
     // at load 1/2 would: the tighter hash sizing only shrinks the rows that hash anyway
     const long long hash_half = (long long)next_pow2(2 * (t < 1 ? 1 : t)) * 16 +
                                 align16((long long)(n > next_pow2(t) ? n : next_pow2(t)) * 8);
+    // (round 5: direct-mapped whenever both fit the small wave bin measured neutral on cop20k-like)
     return num_need_direct(span, n) <= hash_half ? NM_DIRECT : NM_HASH;
 }
 // Wide rows: hash-mode rows whose table would not fit the 256-thread kernel's 64 KiB run

@@ -123,6 +123,33 @@ extern "C" int mhs_diag_setup(int M, unsigned long long** dev) {
 #define MHS_STAMP0()
 #define MHS_STAMP(k)
 #endif
+// Probe guard (diagnostic builds; on with the stamps): a hash probe loop that has visited every
+// slot of its table records where, the key and the table size, and stops -- a key missing from
+// its table would otherwise spin forever (the round-4 stamps run on cage15-like never returned)
+#ifndef MHS_PROBE_GUARD
+#define MHS_PROBE_GUARD MHS_ROW_STAMPS
+#endif
+#if MHS_PROBE_GUARD
+__device__ unsigned long long g_guard[8];  // trips, then the first trip: where, key, H, steps
+__device__ bool probe_guard(int steps, int H, int where, int key) {
+    if (steps <= H) return false;
+    if (atomicAdd(&g_guard[0], 1ull) == 0ull) {
+        g_guard[1] = (unsigned long long)where;
+        g_guard[2] = (unsigned long long)(unsigned)key;
+        g_guard[3] = (unsigned long long)H;
+    }
+    return true;
+}
+extern "C" int mhs_diag_guard(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_guard), sizeof(g_guard));
+}
+#define MHS_GUARD_DECL int guard_steps_ = 0
+#define MHS_GUARD(H, where, key) \
+    if (probe_guard(++guard_steps_, (H), (where), (key))) break
+#else
+#define MHS_GUARD_DECL
+#define MHS_GUARD(H, where, key)
+#endif
 
 namespace mhs {
 
@@ -1739,6 +1766,8 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
         wave_walk(a0, a1, Acol, Aval, bmeta, tiles, work, f);
         return;
     }
+    // (round 5: block rows cut into per-wave pieces of 64-entry chunks, no stage -- webbase-like
+    // +1 %, scircuit-like +3 %, cant-s1-like +4 %: dropped; hub rows are bound by their accumulate)
     for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
                  pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN,
                             tiles ? 1 : (Team::size > 64 ? MHS_UNROLL_BLOCK : MHS_UNROLL)),  // (tile walks: by entries)
@@ -1769,12 +1798,14 @@ struct TileBuild {
             atomicOr(&E[x.tc - lo].mask, x.m);
         } else {
             int s = hslot(x.tc, H);
+            MHS_GUARD_DECL;
             for (;;) {
                 const int old = atomicCAS(&E[s].key, -1, x.tc);
                 if (old == -1 || old == x.tc) {
                     atomicOr(&E[s].mask, x.m);
                     break;
                 }
+                MHS_GUARD(H, 2, x.tc);
                 probe_conflict();
                 s = hnext(s, H);
             }
@@ -1838,7 +1869,9 @@ struct Accum {
             }
             uint4 q = *reinterpret_cast<const uint4*>(&E[s]);  // one ds_read_b128: mask, base, key
             if constexpr (MODE == NM_HASH) {
+                MHS_GUARD_DECL;
                 while ((int)q.w != tc) {
+                    MHS_GUARD(H, 1, tc);
                     probe_conflict();
                     s = hnext(s, H);
                     q = *reinterpret_cast<const uint4*>(&E[s]);
@@ -2032,12 +2065,14 @@ struct SymTileBuild {
             atomicOr(&Mk[x.tc - lo], x.m);
         } else {
             int s = hslot(x.tc, H);
+            MHS_GUARD_DECL;
             for (;;) {
                 const int old = atomicCAS(&Kk[s], -1, x.tc);
                 if (old == -1 || old == x.tc) {
                     atomicOr(&Mk[s], x.m);
                     break;
                 }
+                MHS_GUARD(H, 3, x.tc);
                 probe_conflict();
                 s = hnext(s, H);
             }
@@ -3153,7 +3188,9 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
                 E[key - lo].mask = m;
             } else {
                 int sl = hslot(key, H);
+                MHS_GUARD_DECL;
                 while (atomicCAS(&E[sl].key, -1, key) != -1) {  // keys are distinct
+                    MHS_GUARD(H, 4, key);
                     probe_conflict();
                     sl = hnext(sl, H);
                 }
@@ -4068,7 +4105,7 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     }
 #undef MHS_ANALYZE
 #undef MHS_ANALYZE_LANE
-    if (w.nft_bin) {  // numeric-first probe: the counts go to the host, which picks the bin lists
+    if (w.nft_bin && pub) {  // numeric-first probe: the counts go to the host, which picks the bin lists
         hipLaunchKernelGGL(k_probe_publish, dim3(64), dim3(1024), 0, s, (const unsigned long long*)w.blkflop,
                            G == 1 ? 2 * blocks : blocks,
                            w.stats, pub, seq);

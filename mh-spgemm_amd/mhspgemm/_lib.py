@@ -126,6 +126,9 @@ def lib() -> ctypes.CDLL:
     L.mhs_probe_conflicts.restype = c_int
     L.mhs_ctx_chunked_calls.argtypes = [c_void_p]
     L.mhs_ctx_chunked_calls.restype = ctypes.c_longlong
+    if hasattr(L, "mhs_ctx_stat"):  # (ABI 9)
+        L.mhs_ctx_stat.argtypes = [c_void_p, c_int]
+        L.mhs_ctx_stat.restype = ctypes.c_longlong
     if hasattr(L, "mhs_hbm_peak"):  # (older A/B variant libraries lack the diagnostic)
         L.mhs_hbm_peak.argtypes = [c_void_p, c_size_t, c_int, P(ctypes.c_double)]
         L.mhs_hbm_peak.restype = c_int

@@ -82,6 +82,13 @@ class Tool:
         """Calls that ran row-chunked (the out-of-memory fallback)."""
         return int(L.lib().mhs_ctx_chunked_calls(self.ctx))
 
+    STATS = {"chunked": 0, "split": 1, "sym_fork": 2, "nft": 3, "near": 4, "multi_stream": 5}
+
+    def stat(self, name: str) -> int:
+        """Calls of this context that took a path (mhs_ctx_stat: 'split', 'sym_fork', 'nft',
+        'near', 'multi_stream', 'chunked')."""
+        return int(L.lib().mhs_ctx_stat(self.ctx, self.STATS[name]))
+
     def hbm_peak(self, nbytes: int = 2 << 30, iters: int = 10) -> dict:
         """Measured HBM bandwidth of this device (GB/s): copy (read + write bytes), read,
         write streaming kernels over `nbytes` buffers (mhs_hbm_peak)."""

@@ -697,3 +697,68 @@ def test_numeric_first_tiny_rows(tool, slots, monkeypatch):
     finally:
         t2.close()
 
+
+
+# ---- round 5: path counters (mhs_ctx_stat) assert that the rarer paths actually ran ----------
+
+def test_split_block_bins_ran(tool):
+    """block bins split by LDS need (k_split_bins, from 2^24 products, numeric launches
+    over several streams) -- webbase-like holds 256-thread block rows on both sides of the split;
+    the split launches must run and the product equal the oracle's."""
+    A = synth.SYNTH["webbase-1M"]()
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        t = check(t2, A, A)
+        assert t.flop >= 1 << 24
+        assert t2.stat("multi_stream") == 1 and t2.stat("split") == 1, (t2.stat("split"), t.num_bins)
+    finally:
+        t2.close()
+        A.d_release_csr()
+
+
+@pytest.mark.parametrize("fork", ["0", "1"])
+def test_near_groups_with_symbolic_fork(tool, fork, monkeypatch):
+    """the rare symbolic bins on an aux stream (MHS_SYM_FORK=1) with near groups on:
+    the near check then runs in launch_near after the aux stream's join -- verified groups and
+    the oracle's C either way; the non-finite dissolve on the forked ordering too."""
+    monkeypatch.setenv("MHS_SYM_FORK", fork)
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        A = _perturbed_fem(7, 6, 24, 0.03, seed=31)
+        t = check(t2, A, A)
+        assert t.num_bins[6] + t.num_bins[7] > 0, t.num_bins
+        assert t2.stat("near") == 1
+        assert t2.stat("sym_fork") == (1 if fork == "1" else 0)
+        v = A.val.copy()
+        v[[5, 1000, 2500]] = np.inf
+        v[4321] = np.nan
+        An = mhspgemm.CSR(A.M, A.N, A.ptr, A.col, v)
+        p, c, vv, _ = run_gpu(t2, An, An)
+        Cp, Ci, Cv = orc.spgemm(An.ptr, An.col, An.val, An.ptr, An.col, An.val, An.N)
+        assert np.array_equal(p, Cp) and np.array_equal(c, Ci)
+        assert np.array_equal(np.isnan(vv), np.isnan(Cv)) and np.array_equal(np.isinf(vv), np.isinf(Cv))
+        fin = np.isfinite(Cv)
+        assert np.allclose(vv[fin], Cv[fin], rtol=RTOL, atol=ATOL)
+    finally:
+        t2.close()
+
+
+@pytest.mark.parametrize("auto", ["12", "0"])
+def test_numeric_first_without_probe(tool, auto, monkeypatch):
+    """Round 5: short-row matrices below the probe's 512 K rows sort their tiny rows once, in
+    symbolic, into value slots sized by the per-row bound (no hand-off); MHS_NFT_AUTO_AVG=0 keeps
+    the two sorts.  Same C either way, on the tiny zoo and the short-row configs."""
+    monkeypatch.setenv("MHS_NFT_AUTO_AVG", auto)
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = tiny_zoo(7)
+        A = mhspgemm.CSR(M, K, Ap, Ac, Av)
+        B = mhspgemm.CSR(K2, N, Bp, Bc, Bv)
+        check(t2, A, B)
+        for name in ("mac_econ_fwd500", "scircuit"):
+            A = synth.SYNTH[name]()
+            check(t2, A, A)
+            A.d_release_csr()
+        assert (t2.stat("nft") > 0) == (auto != "0"), t2.stat("nft")
+    finally:
+        t2.close()

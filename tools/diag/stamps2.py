@@ -4,7 +4,7 @@ import sys, ctypes, os, time
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "mh-spgemm_amd")]
-os.environ["MHS_LIB"] = str(ROOT / "tools/diag/v9/libmhspgemm.so")
+os.environ["MHS_LIB"] = os.environ.get("STAMPS_LIB", str(ROOT / "tools/diag/v9/libmhspgemm.so"))
 import numpy as np, torch
 from mhspgemm import _lib
 import mhspgemm
@@ -18,9 +18,13 @@ tool = mhspgemm.Tool(0)
 L = _lib.lib(); L.mhs_diag_setup.argtypes = [ctypes.c_int, ctypes.c_void_p]
 dev = ctypes.c_void_p()
 assert L.mhs_diag_setup(A.M, ctypes.byref(dev)) == 0
+g = (ctypes.c_ulonglong * 8)()
 for i in range(3):
     C, t = mhspgemm.spgemm(tool, A, A); C.release()
     print(f"[{time.time()-t0:.1f}s] call {i}: numeric {t.Numeric:.3f} ms", flush=True)
+    if hasattr(L, "mhs_diag_guard"):  # probe-guard trips (a key missing from its hash table)
+        L.mhs_diag_guard(g)
+        print(f"  probe guard: trips {g[0]} first: where {g[1]} key {g[2]} H {g[3]}", flush=True)
 buf = np.zeros(A.M * 8, np.uint64)
 assert L.mhs_memcpy(tool.ctx, ctypes.c_void_p(buf.ctypes.data), dev, buf.nbytes, 1) == 0
 ph = buf.reshape(A.M, 8).astype(np.float64)
