@@ -293,6 +293,7 @@ def main():
                     "frac_numeric": round(bcm / (avg_n * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                     "frac_e2e": round(bcm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                     "_frac_e2e": bcm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                    "suitesparse_stats": synth.TARGETS.get(m),
                     "phases_ms": {k: round(getattr(tm, k), 4) for k in (
                         "Form_mask_matrix_B", "symbolic_binning", "Calculate_C_nnz", "numeric_binning", "Numeric",
                         "total_e2e")},

@@ -119,9 +119,35 @@ extern "C" int mhs_diag_setup(int M, unsigned long long** dev) {
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_rowdiag), dev, sizeof(void*));
     return (int)e;
 }
+// symbolic rows (sym_row_s): [M][4] phases -- clear, tile walk, count, row cache / spill list
+__device__ unsigned long long* g_symdiag;
+extern "C" int mhs_diag_setup_sym(int M, unsigned long long** dev) {
+    hipError_t e = hipMalloc((void**)dev, (size_t)M * 32);
+    if (e == hipSuccess) e = hipMemset(*dev, 0, (size_t)M * 32);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_symdiag), dev, sizeof(void*));
+    return (int)e;
+}
+#define MHS_SSTAMP0() unsigned long long tps_ = __builtin_amdgcn_s_memtime()
+#define MHS_SSTAMP(k)                                                     \
+    do {                                                                  \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();      \
+        if (tm.rank() == 0 && g_symdiag) g_symdiag[(size_t)row * 4 + (k)] = t_ - tps_; \
+        tps_ = t_;                                                        \
+    } while (0)
 #else
 #define MHS_STAMP0()
 #define MHS_STAMP(k)
+#define MHS_SSTAMP0()
+#define MHS_SSTAMP(k)
+#endif
+// (bisecting the round-4/5 stamps hang on cage15-like: MHS_STAMP_NUM_BODY=0 keeps the stamps out
+// of num_row_body, the wave and 256-thread rows)
+#if MHS_ROW_STAMPS && defined(MHS_STAMP_NUM_BODY) && !MHS_STAMP_NUM_BODY
+#define MHS_BSTAMP0()
+#define MHS_BSTAMP(k)
+#else
+#define MHS_BSTAMP0() MHS_STAMP0()
+#define MHS_BSTAMP(k) MHS_STAMP(k)
 #endif
 // Probe guard (diagnostic builds; on with the stamps): a hash probe loop that has visited every
 // slot of its table records where, the key and the table size, and stops -- a key missing from
@@ -2100,6 +2126,7 @@ __device__ __forceinline__ void sym_row(const Team& tm, const SymArgs& a, int ro
 template <class Team>
 __device__ void sym_row_s(const Team& tm, const SymArgs& a, const SymRow& r, TileEntry* E, int4* stage) {
     const int row = r.row, lo = r.lo, hi = r.hi, tflop = r.tflop;
+    MHS_SSTAMP0();
     const int span = hi - lo + 1;
     const bool direct = sym_direct(span, tflop);
     const int H = direct ? span : hash_slots(tflop < span ? tflop : span);
@@ -2110,9 +2137,11 @@ __device__ void sym_row_s(const Team& tm, const SymArgs& a, const SymRow& r, Til
         if (!direct) Kk[s] = -1;
     }
     tm.sync();
+    MHS_SSTAMP(0);
     walk_products(tm, r.a0, r.a1, a.Acol, nullptr, a.bmeta, true, tflop,
                   SymTileBuild{Mk, Kk, direct, lo, H, a.btcol, a.btmask}, stage);
     tm.sync();
+    MHS_SSTAMP(1);
     long long n = 0;
     int t = 0;
     for (int s = tm.rank(); s < H; s += Team::size) {
@@ -2122,6 +2151,7 @@ __device__ void sym_row_s(const Team& tm, const SymArgs& a, const SymRow& r, Til
     }
     n = tm.sum(n);
     t = tm.sum(t);
+    MHS_SSTAMP(2);
     const int R = __builtin_amdgcn_readfirstlane((int)a.grp[row]);  // the group's rows share the pattern
     if (tm.rank() < R) {
         a.Cptr[row + tm.rank()] = (int)n;
@@ -2186,6 +2216,7 @@ __device__ void sym_row_s(const Team& tm, const SymArgs& a, const SymRow& r, Til
         }
     }
     tm.sync();
+    MHS_SSTAMP(3);
 }
 
 // the small-table wave bin, blocks [0, nb) of a grid
@@ -3116,7 +3147,7 @@ template <class Team, bool GLOBALMEM, int MODE, bool GROUPED, bool O32>
 __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, int row, int lo, int span, int t,
                              int c0, int n, int a0, int a1, char* region, int* counter,
                              int4* stage, int R) {
-    MHS_STAMP0();
+    MHS_BSTAMP0();
     const int H = MODE == NM_HASH ? hash_slots(t) : span;
     const int colbase = lo << TILE_SHIFT;
     TileEntry* E = (TileEntry*)region;
@@ -3146,7 +3177,7 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
     }
     // 1. the C row's tile table: the symbolic pass's masks when it kept them,
     //    else rebuilt (same OR pass as symbolic)
-    MHS_STAMP(0);
+    MHS_BSTAMP(0);
     // symbolic kept the masks unless it sorted the row as a tiny one (numeric runs those
     // with tables when the tiny classes are off: N beyond the packed keys' 23 bits)
     const bool sym_tiny = tiny_class_sym(__builtin_amdgcn_readfirstlane(a.rflop[row]), a1 - a0) >= 0;
@@ -3208,7 +3239,7 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
                     tflop, stage);
         tm.sync();
     }
-    MHS_STAMP(1);
+    MHS_BSTAMP(1);
 
     if constexpr (GROUPED) group_pair_meta(gp, a.bmeta);
     // 2. rank of every tile's first column = prefix popcount in tile order
@@ -3306,10 +3337,10 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
             [&](int e, int v) { E[(int)(unsigned)S[e]].base = v; });
     }
     tm.sync();
-    MHS_STAMP(2);
+    MHS_BSTAMP(2);
     for (int r = tm.rank(); r < nclear; r += Team::size) acc[r] = 0.0;
     tm.sync();
-    MHS_STAMP(3);
+    MHS_BSTAMP(3);
 
     // 3. accumulate every product of the row (of the group's rows)
     {
@@ -3327,7 +3358,7 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
         }
     }
     tm.sync();
-    MHS_STAMP(4);
+    MHS_BSTAMP(4);
 
     // 4. write C (sorted by construction: tiles in column order, bits in order)
     if constexpr (MODE == NM_DENSE) {
@@ -3360,7 +3391,7 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
         store_cols(a.Ccol + c0, cb, n, GROUPED ? R : 1, tm.rank(), Team::size);
     }
     tm.sync();
-    MHS_STAMP(5);
+    MHS_BSTAMP(5);
 }
 
 // Row-level scalars are made provably wave-uniform (readfirstlane) so that the

@@ -232,3 +232,18 @@ def test_mtx_cache_env_words(tmp_path, monkeypatch):
     A = mhspgemm.CSR()
     assert mhspgemm.readMtxFile(A, str(f)) == 0 and A.nnz == 2
     assert not (tmp_path / "false").exists() and not (tmp_path / "m.mtx.mhscsr").exists()
+
+
+@pytest.mark.parametrize("name", ["webbase-1M", "cop20k_A"])
+def test_standin_stats(name):
+    """the stand-ins recalibrated to SURVEY §8's SuiteSparse statistics --
+    the counts synth.ACHIEVED records hold, and they are within 20 % of synth.TARGETS."""
+    from mhspgemm import synth
+    A = synth.SYNTH[name]()
+    bl = np.diff(A.ptr).astype(np.int64)
+    got = dict(M=A.M, nnzA=A.nnz, flop=int(bl[A.col].sum()), max_row=int(bl.max()))
+    rec, tgt = synth.ACHIEVED[name], synth.TARGETS[name]
+    for k, v in got.items():
+        assert v == rec[k], (k, v, rec[k])
+    for k in ("nnzA", "flop", "nnzC", "max_row"):
+        assert abs(rec[k] / tgt[k] - 1) <= 0.2, (k, rec[k], tgt[k])

@@ -18,6 +18,10 @@ tool = mhspgemm.Tool(0)
 L = _lib.lib(); L.mhs_diag_setup.argtypes = [ctypes.c_int, ctypes.c_void_p]
 dev = ctypes.c_void_p()
 assert L.mhs_diag_setup(A.M, ctypes.byref(dev)) == 0
+sdev = ctypes.c_void_p()
+if hasattr(L, "mhs_diag_setup_sym"):  # symbolic rows' phases (sym_row_s)
+    L.mhs_diag_setup_sym.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    assert L.mhs_diag_setup_sym(A.M, ctypes.byref(sdev)) == 0
 g = (ctypes.c_ulonglong * 8)()
 for i in range(3):
     C, t = mhspgemm.spgemm(tool, A, A); C.release()
@@ -63,3 +67,17 @@ print("slowest rows: row, total cycles (ms at 2.4 GHz), flop, nA, phases")
 for r in order:
     print(f"  {r:9d} {tot_r[r]:12.0f} ({tot_r[r] / 2.4e6:.3f} ms) flop {rf[r]:9d} nA {nA[r]:6d} ",
           " ".join(f"{ph[r, k]:.0f}" for k in range(6)))
+
+if sdev.value:
+    sb = np.zeros(A.M * 4, np.uint64)
+    assert L.mhs_memcpy(tool.ctx, ctypes.c_void_p(sb.ctypes.data), sdev, sb.nbytes, 1) == 0
+    sp_ = sb.reshape(A.M, 4).astype(np.float64)
+    srow = sp_.sum(1) > 0
+    snames = ["clear", "tile walk", "count", "cache/spill"]
+    print("symbolic table rows", srow.sum(), "of", A.M)
+    for k, nm in enumerate(snames):
+        print(f"  {nm:12s} {sp_[srow, k].mean():10.0f} cycles/row")
+    tot_s = sp_.sum(1)
+    print("slowest symbolic rows: row, total cycles, flop, nA, phases")
+    for r in np.argsort(-tot_s)[:10]:
+        print(f"  {r:9d} {tot_s[r]:12.0f} flop {rf[r]:9d} nA {nA[r]:6d} ", " ".join(f"{sp_[r, k]:.0f}" for k in range(4)))
