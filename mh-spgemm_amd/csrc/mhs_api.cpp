@@ -372,13 +372,16 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
     const int nl = numeric_launches(h);
     const int nss = (nl >= 3 && h.flop >= (1ull << MHS_MULTI_FLOP_LOG2)) ? std::min(ctx->num_streams, nl) : 1;
+    hipError_t fe = hipSuccess;
     if (nss > 1) {
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
-        for (int i = 1; i < nss; ++i) {
-            ss[i] = ctx->aux[i - 1];
-            MHS_HIP(hipStreamWaitEvent(ss[i], ctx->fork_ev, 0));
-        }
+        for (int i = 1; i < nss; ++i) ss[i] = ctx->aux[i - 1];
     }
+    // the aux streams wait for the fork (everything before numeric) -- set up after the first
+    // numeric launch has gone out on the call's stream (launch_numeric)
+    auto fork = [&]() {
+        for (int i = 1; i < nss && fe == hipSuccess; ++i) fe = hipStreamWaitEvent(ss[i], ctx->fork_ev, 0);
+    };
     // block bins split by LDS need only where their two launches can run side by side (on
     // one stream the hub rows' launch would no longer overlap the others' bulk).  The partition
     // runs on the call's stream after the fork: only the split launches wait for it (split_ev),
@@ -391,7 +394,9 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     ctx->stat[MHS_STAT_SPLIT] += split;
     ctx->stat[MHS_STAT_MULTI_STREAM] += nss > 1;
     const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
-                                    ctx->dense_span_max, split, split ? ctx->split_ev : nullptr);
+                                    ctx->dense_span_max, split, split ? ctx->split_ev : nullptr,
+                                    nss > 1 ? std::function<void()>(fork) : std::function<void()>());
+    MHS_HIP(fe);
     MHS_HIP(hipGetLastError());
     for (int i = 1; i < nss; ++i)
         if (used & (1 << i)) {

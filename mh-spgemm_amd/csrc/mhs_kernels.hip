@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <climits>
 #include <functional>
+#include <type_traits>
 #include <vector>
 
 #ifndef MHS_ROW_STAMPS
@@ -1778,6 +1779,83 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
     }
 }
 
+// Block teams of 1024 threads, per-wave pieces (round 5, MHS_PIECES): the row's A entries cut
+// into 16 contiguous pieces, each wave walking its own in 64-entry chunks with a lane-group width
+// per chunk, no stage and no barrier.  The staged walk above runs lane groups of at least T/64
+// lanes, so at most 64 A entries per dependent load round trip and S of them in sequence per
+// barrier: webbase-like's hub rows (4,400 entries of ~4 products) took ~84 round trips a walk
+// (row stamps: ~170 k cycles per walk).  The group width counts the chunk's longest segment too
+// (a hub column's long B row among short ones).  (For the 256-thread kernels the pieces measured
+// slower: scircuit-like +3 %, cant-s1-like +4 %.)
+#ifndef MHS_PIECES
+#define MHS_PIECES 1
+#endif
+// (round 5: single wave rows' first A chunk loaded before the tile table, as row groups do --
+// cage15-like +5 %, offshore-like +10 %, cop20k-like +4 %: the 5 KiB hash kernel spills at 8 waves)
+#ifndef MHS_PIECE_UNROLL
+#define MHS_PIECE_UNROLL 2  // B entries per lane issued together in a piece's value walk (registers)
+#endif
+__device__ __forceinline__ int chunk_group_mx(int nh, int avg, int mx, int U, int gmin) {
+    int best = gmin, bc = INT_MAX;
+    for (int g = gmin; g <= 64; g <<= 1) {
+        const int ng = 64 / g;
+        const int c0 = ((nh + ng - 1) / ng) * ((avg + g * U - 1) / (g * U));
+        const int c1 = (mx + g * U - 1) / (g * U);
+        const int c = c0 > c1 ? c0 : c1;
+        if (c <= bc) {
+            bc = c;
+            best = g;
+        }
+    }
+    return best;
+}
+template <int T, class F>
+__device__ __forceinline__ void for_products_pieces(int a0, int a1, const int* __restrict__ Acol,
+                                                    const double* __restrict__ Aval, const int4* __restrict__ bmeta,
+                                                    bool tiles, int avg, const F& f) {
+    constexpr int NW = T / 64;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nA = a1 - a0;
+    const int p0 = a0 + (int)((long long)nA * wv / NW), p1 = a0 + (int)((long long)nA * (wv + 1) / NW);
+    const int lane = lane_id();
+    const int U = tiles ? MHS_TILE_UNROLL : MHS_PIECE_UNROLL;
+    for (int jb = p0; jb < p1; jb += 64) {
+        ChunkLoads c = load_chunk_a(lane, jb, p1, Acol, Aval);
+        load_chunk_meta(c, bmeta);
+        // every entry its own visit (no run sweeps: the 1024-thread kernels' registers)
+        StagedChunk x;
+        x.st = c.in ? c.m.x : 0;
+        x.ln = c.in ? (tiles ? meta_ntiles(c.m) : c.m.y) : 0;
+        x.av = c.av;
+        const unsigned long long Hm = __ballot(c.in);
+        x.nh = __popcll(Hm);
+        const int mx = wave_max(x.ln);
+        const int G = chunk_group_mx(x.nh, avg, mx, U, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN);
+        const int gs = 31 - __clz(G);  // G is a power of two
+        const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
+        const int iters = (x.nh + ngrp - 1) / ngrp;
+        for (int it = 0; it < iters; ++it) {
+            const int e = grp * iters + it;  // (entries in lane order: the chunk's lanes [0, nh) hold them)
+            const int st = __shfl(x.st, e & 63);
+            const int n0 = __shfl(x.ln, e & 63);
+            const double av = __shfl(x.av, e & 63);
+            const int n = e < x.nh ? n0 : 0;
+            if constexpr (F::kValues) {
+                const double avs[1] = {av};
+                run_segment_run<1, MHS_PIECE_UNROLL>(f, st, n, gl, G, avs, 1);
+            } else {
+                run_segment(f, st, n, gl, G, 0.0);
+            }
+        }
+    }
+}
+struct WideTiles;
+struct WideAccum;
+template <class F>
+__device__ constexpr bool piece_walk_ok() {
+    return MHS_PIECES && !std::is_same<F, WideTiles>::value && !std::is_same<F, WideAccum>::value;
+}
+
 // Lane groups (a flattened walk -- 64 consecutive products per batch, the owner of each
 // found by a search over the chunk's prefix of segment lengths -- measured slower: its
 // per-batch owner search costs more instructions than it saves in coalescing).
@@ -1792,8 +1870,13 @@ __device__ __forceinline__ void walk_products(const Team& tm, int a0, int a1,
         wave_walk(a0, a1, Acol, Aval, bmeta, tiles, work, f);
         return;
     }
-    // (round 5: block rows cut into per-wave pieces of 64-entry chunks, no stage -- webbase-like
-    // +1 %, scircuit-like +3 %, cant-s1-like +4 %: dropped; hub rows are bound by their accumulate)
+    if constexpr (Team::size >= 1024 && piece_walk_ok<F>()) {
+        const int avg = nA > 0 ? (int)((work + nA - 1) / nA) : 1;
+        if (nA >= 2 * Team::size) {  // (rows of at least two 64-entry chunks a wave)
+            for_products_pieces<Team::size>(a0, a1, Acol, Aval, bmeta, tiles, avg, f);
+            return;
+        }
+    }
     for_products(tm, a0, a1, Acol, Aval, bmeta, tiles,
                  pick_group(work, nA, Team::size, tiles ? MHS_TILE_GMIN : MHS_VAL_GMIN,
                             tiles ? 1 : (Team::size > 64 ? MHS_UNROLL_BLOCK : MHS_UNROLL)),  // (tile walks: by entries)
@@ -4477,7 +4560,7 @@ struct NumLaunch {
 
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
                    double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max, bool split,
-                   hipEvent_t split_ev) {
+                   hipEvent_t split_ev, const std::function<void()>& fork) {
     std::vector<NumLaunch> L;
     auto add = [&](std::function<void(hipStream_t)> go) { L.push_back(NumLaunch{std::move(go)}); };
     NumArgs a{};
@@ -4701,13 +4784,19 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             else hipLaunchKernelGGL((k_num_wave_direct<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
         });
     }
+    // launch i on ss[i % n]: the first (largest rows) goes out on the call's stream at once, and the
+    // aux streams' waits on the fork event are set up after it (`fork`, host API calls that would
+    // otherwise sit between the hand-off and the first numeric kernel: round 5, scircuit-like's
+    // hand-off gap 46 -> ? us)
     int used = 0;
     const int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
     for (size_t i = 0; i < L.size(); ++i) {
-        const int k = n > 1 ? (int)((i + 1) % n) : 0;
+        const int k = n > 1 ? (int)(i % n) : 0;
+        if (i == 1 && n > 1 && fork) fork();
         used |= 1 << k;
         L[i].go(ss[k]);
     }
+    if (L.size() <= 1 && n > 1 && fork) fork();  // (the caller's joins expect the fork)
     return used;
 }
 }  // namespace mhs
