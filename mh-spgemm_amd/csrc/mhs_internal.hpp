@@ -61,8 +61,8 @@ constexpr int TINY_NUM_NMAX = (1 << 23) - 1;  // ... so a numeric tiny row spans
 // class 0 were slower or neutral.
 __host__ __device__ constexpr int tiny_w(int c) { return 4 << (c < 4 ? c : 4); }  // 4 8 16 32 64 64
 __host__ __device__ constexpr int tiny_k(int c) { return c == 0 ? 2 : c == 5 ? 8 : 4; }
-__host__ __device__ constexpr int tiny_ws(int c) { return c <= 2 ? 8 : 32; }
-__host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? 1 : c == 2 ? 8 : 4; }
+__host__ __device__ constexpr int tiny_ws(int c) { return c <= 2 ? 8 : c == 3 ? 32 : 64; }
+__host__ __device__ constexpr int tiny_ks(int c) { return c == 0 ? 1 : (c == 2 || c == 4) ? 8 : 4; }
 constexpr int TINY_FUSED_KMAX = 4;  // largest K of the numeric classes 0..3 (one fused launch)
 constexpr int TINY_SLOT_MAX = 128;  // value slots of a numeric-first row: W*K of its class (0..3), at most 32*4
 // Symbolic uses the classes below TINY_SYM_NC only (past 128 products a hash table
@@ -70,6 +70,13 @@ constexpr int TINY_SLOT_MAX = 128;  // value slots of a numeric-first row: W*K o
 // would not fit the small wave bin (measured: cop20k-like 2.3x slower sorted, while
 // rows that need big tables run 2x faster sorted).
 constexpr int TINY_SYM_NC = 4;
+// ... except scattered rows: symbolic class 4, (64,8), takes rows of at most 512 products that
+// the small wave table cannot hold (k_analyze's sym_tiny_class: a hub column's B row in the
+// row, web-graph rows), which otherwise count in 10 KiB waves or block tables
+constexpr int TINY_SYMX_NC = 5;
+#ifndef MHS_SYM_SORT64
+#define MHS_SYM_SORT64 1
+#endif
 #ifndef MHS_TINY_NUM_SMALL
 #define MHS_TINY_NUM_SMALL 4
 #endif

@@ -1020,6 +1020,19 @@ __device__ __forceinline__ int sym_bin_of(int flop, int tflop, int span) {
     return SYM_GLOBAL;
 }
 
+// A row's symbolic tiny class (-1: none): tiny_class_sym's 8- and 32-lane classes, and class 4
+// -- (64,8), a register sort of at most 512 products -- for a row the small wave table cannot
+// hold (round 5: such rows -- a hub column's B row beside a few short ones, web-graph rows of
+// a few hundred scattered tiles -- took 2-4 dependent table steps a product in 10 KiB waves
+// or block tables).  Numeric recomputes it to know which rows left no masks behind.
+__device__ __forceinline__ int sym_tiny_class(int flop, int nA, int tflop, int span) {
+    const int c = tiny_class_sym(flop, nA);
+    if (MHS_SYM_SORT64 && c < 0 && flop > 0 && flop <= tiny_ws(4) * tiny_ks(4) && nA <= tiny_ws(4) &&
+        sym_bin_of(flop, tflop, span) != SYM_WAVE)
+        return 4;
+    return c;
+}
+
 // Stats -> fine-grained pinned host memory, then the sequence number the host spins
 // on (wave 0 of one block: L1-bypassing reads, system-scope stores, release of the
 // number).  One wave does it all, so the release's wait for the wave's outstanding
@@ -1061,7 +1074,7 @@ __device__ __forceinline__ void analyze_out(int row, long long flop, long long t
                                             int* __restrict__ ctiles, unsigned char* __restrict__ sym_bin,
                                             int* __restrict__ Cptr, unsigned char* __restrict__ asame,
                                             unsigned char* __restrict__ nft_bin, int& nslots, int& nother,
-                                            unsigned* __restrict__ nsig);
+                                            unsigned* __restrict__ nsig, int sort64);
 template <int G, int U = (G == 64 ? 4 : 1)>
 __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, const int* __restrict__ Aptr,
                                                  const int* __restrict__ Acol, const int4* __restrict__ bmeta,
@@ -1071,7 +1084,7 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
                                                  unsigned char* __restrict__ sym_bin, int* __restrict__ Cptr,
                                                  unsigned char* __restrict__ asame, int& err,
                                                  unsigned char* __restrict__ nft_bin, int& nslots, int& nother,
-                                                 unsigned* __restrict__ nsig) {
+                                                 unsigned* __restrict__ nsig, int sort64) {
     const int gl = lane_id() & (G - 1);
     long long flop = 0, tflop = 0;
     int lo = INT_MAX, hi = -1;
@@ -1137,7 +1150,7 @@ __device__ __forceinline__ long long analyze_row(int row, bool valid, int MB, co
     }
     if (valid && gl == 0)
         analyze_out(row, flop, tflop, lo, hi, kfirst, differ, bad, Aptr[row + 1] - Aptr[row], rflop, rtflop, rlo, rhi,
-                    ctiles, sym_bin, Cptr, asame, nft_bin, nslots, nother, nsig);
+                    ctiles, sym_bin, Cptr, asame, nft_bin, nslots, nother, nsig, sort64);
     return valid ? flop : 0;
 }
 
@@ -1148,7 +1161,7 @@ __device__ __forceinline__ void analyze_out(int row, long long flop, long long t
                                             int* __restrict__ ctiles, unsigned char* __restrict__ sym_bin,
                                             int* __restrict__ Cptr, unsigned char* __restrict__ asame,
                                             unsigned char* __restrict__ nft_bin, int& nslots, int& nother,
-                                            unsigned* __restrict__ nsig) {
+                                            unsigned* __restrict__ nsig, int sort64) {
     {
         // a row with an out-of-range column enters no bin: the symbolic kernels gather
         // bmeta[Acol[j]] unchecked, and the host returns MHS_ERR_INVALID before numeric
@@ -1159,7 +1172,10 @@ __device__ __forceinline__ void analyze_out(int row, long long flop, long long t
         rtflop[row] = tf;
         rlo[row] = lo;
         rhi[row] = hi;
-        const int tc = tiny_class_sym(f, nA);
+        // (class 4 only where numeric sorts the row too: k_scan sends it to a 64-lane tiny class,
+        // so no numeric table kernel looks for masks symbolic did not keep)
+        const int tc = sort64 && (long long)span * TILE_BITS - 1 <= TINY_NUM_NMAX ? sym_tiny_class(f, nA, tf, span)
+                                                                                   : tiny_class_sym(f, nA);
         const int bin = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
         // near row-group signature (k_bin_list links rows whose signatures match: the same
@@ -1175,7 +1191,8 @@ __device__ __forceinline__ void analyze_out(int row, long long flop, long long t
             // numeric-first candidates: the numeric classes 0..3, whose sort keys hold the
             // column relative to the row's first tile (23 bits); a wider row counts in a table
             const int tn = (long long)span * TILE_BITS - 1 <= TINY_NUM_NMAX ? tiny_class(f, nA, TINY_SYM_NC) : -1;
-            nft_bin[row] = (unsigned char)(tn >= 0 ? SYM_TINY + tn : tc >= 0 ? sym_bin_of(f, tf, span) : bin);
+            // (class 4 rows sort in symbolic's class-4 range either way)
+            nft_bin[row] = (unsigned char)(tn >= 0 ? SYM_TINY + tn : tc >= 0 && tc < 4 ? sym_bin_of(f, tf, span) : bin);
             nslots += tn >= 0 ? tiny_w(tn) * tiny_k(tn) : 0;
             nother += f > 0 && tn < 0;
         }
@@ -1206,7 +1223,7 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
                                                  unsigned char* __restrict__ asame,
                                                  Stats* __restrict__ stats,
                                                  unsigned long long* __restrict__ lb_state, int nlb,
-                                                 unsigned char* __restrict__ nft_bin, unsigned* __restrict__ nsig) {
+                                                 unsigned char* __restrict__ nft_bin, unsigned* __restrict__ nsig, int sort64) {
     const int lane = lane_id();
     const int gl = lane & (G - 1);
     const int row = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
@@ -1217,13 +1234,13 @@ __global__ __launch_bounds__(256) void k_analyze(int M, int MB, const int* __res
     bool lng = false;
     if constexpr (G < 64) lng = valid && Aptr[row + 1] - Aptr[row] > AN_LONG * G;
     long long flop = analyze_row<G, U>(row, valid && !lng, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
-                                    ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig);
+                                    ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig, sort64);
     flop = gl == 0 ? flop : 0;
     if constexpr (G < 64) {
         for (unsigned long long lb = __ballot(lng && gl == 0); lb; lb &= lb - 1) {
             const int r = __shfl(row, __builtin_ctzll(lb));
             const long long f = analyze_row<64>(r, true, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi,
-                                                ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig);
+                                                ctiles, sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig, sort64);
             flop += lane == 0 ? f : 0;
         }
     }
@@ -1256,7 +1273,7 @@ __global__ __launch_bounds__(256) void k_analyze_lane(int M, int MB, const int* 
                                                       unsigned long long* __restrict__ blkflop,
                                                       unsigned char* __restrict__ asame, Stats* __restrict__ stats,
                                                       unsigned long long* __restrict__ lb_state, int nlb,
-                                                      unsigned char* __restrict__ nft_bin, unsigned* __restrict__ nsig) {
+                                                      unsigned char* __restrict__ nft_bin, unsigned* __restrict__ nsig, int sort64) {
     const int lane = lane_id();
     const int row = (int)(blockIdx.x * 256u + threadIdx.x);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nlb; i += gridDim.x * blockDim.x)
@@ -1316,12 +1333,12 @@ __global__ __launch_bounds__(256) void k_analyze_lane(int M, int MB, const int* 
     }
     if (act)
         analyze_out(row, flop, tflop, lo, hi, kfirst, differ, bad, len, rflop, rtflop, rlo, rhi, ctiles, sym_bin,
-                    Cptr, asame, nft_bin, nslots, nother, nsig);
+                    Cptr, asame, nft_bin, nslots, nother, nsig, sort64);
     if (!act) flop = 0;
     for (unsigned long long lb = __ballot(lng); lb; lb &= lb - 1) {
         const int r = __shfl(row, __builtin_ctzll(lb));
         const long long f = analyze_row<64>(r, true, MB, Aptr, Acol, bmeta, bhi, rflop, rtflop, rlo, rhi, ctiles,
-                                            sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig);
+                                            sym_bin, Cptr, asame, err, nft_bin, nslots, nother, nsig, sort64);
         flop += lane == 0 ? f : 0;
     }
     __shared__ unsigned long long wsum[4];
@@ -2905,7 +2922,8 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                int dense_span_max, Published* pub, int seq, int tiny_ok,
                                                const unsigned long long* __restrict__ blkflop, int nflop, int nft,
                                                long long* __restrict__ tslot, const int* __restrict__ gna,
-                                               int4* __restrict__ bmeta_near) {
+                                               int4* __restrict__ bmeta_near,
+                                               const unsigned char* __restrict__ sym_bin) {
     constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
     static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
@@ -2935,7 +2953,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         const int i1 = min(nflop, (bid + 1) * per);
         for (int i = bid * per + threadIdx.x; i < i1; i += 1024) fpart += blkflop[i] & BLK_FLOP_MASK;
     }
-    int v[PER], rlo_k[PER], rhi_k[PER], grp_k[PER], a0_k[PER], a1_k[PER], rfl_k[PER], ctl_k[PER];
+    int v[PER], rlo_k[PER], rhi_k[PER], grp_k[PER], a0_k[PER], a1_k[PER], rfl_k[PER], ctl_k[PER], sb_k[PER];
     auto row_scalars = [&]() {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
@@ -2948,6 +2966,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
             a1_k[k] = in ? Aptr[i + 1] : 0;
             rfl_k[k] = in ? rflop[i] : 0;
             ctl_k[k] = in ? ctiles[i] : 0;
+            sb_k[k] = in ? sym_bin[i] : 0;
         }
     };
     long long loc = 0;
@@ -3008,11 +3027,14 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
             const bool tok = tiny_ok && (long long)span * TILE_BITS - 1 <= TINY_NUM_NMAX;
             // numeric-first rows (k_analyze's rule) have their values: one copy list
             const int fc = nft && tok ? tiny_class(rfl_k[k], nA, TINY_SYM_NC) : -1;
+            // symbolic's scattered class (k_analyze allows it only where tok holds) kept no masks:
+            // the row sorts in numeric too, on its own (a group's rows are all of the class)
+            const bool s4 = sb_k[k] == SYM_TINY + 4;
             const int gb =
-                fc >= 0 ? -1 : num_group_bin_of(n, hflop, span, ctl_k[k], gh, dense_span_max, hnA, tok);
+                fc >= 0 || s4 ? -1 : num_group_bin_of(n, hflop, span, ctl_k[k], gh, dense_span_max, hnA, tok);
             if (nft && fc < 0) tslot[i] = -1;  // (slot rows: written by the symbolic pass)
             if (gb < 0)
-                nbin = NUM_TINY + fc;
+                nbin = NUM_TINY + (s4 ? tiny_class(rfl_k[k], nA) : fc);
             else if (gb != NUM_NONE)
                 nbin = (g & GRP_CONT) ? NUM_NONE : gb;
             else
@@ -3263,6 +3285,7 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
     MHS_BSTAMP(0);
     // symbolic kept the masks unless it sorted the row as a tiny one (numeric runs those
     // with tables when the tiny classes are off: N beyond the packed keys' 23 bits)
+    // (symbolic's class 4 rows never come here: k_scan sorts them in numeric too)
     const bool sym_tiny = tiny_class_sym(__builtin_amdgcn_readfirstlane(a.rflop[row]), a1 - a0) >= 0;
     const int lofs = (a.mcache && !sym_tiny && spill_row(span, tflop, t, a.mc_list))
                          ? __builtin_amdgcn_readfirstlane(a.sp.lofs[row])
@@ -3290,11 +3313,13 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
         // symbolic's compacted list of the t (key, mask) pairs (the row-cache slot, or a spill
         // list); a hashed row that ranks by counting also gets its (key, slot | popc) list
         // here, no table compaction later
+        const unsigned long long* slot = lofs >= 0 ? a.sp.mask + lofs : a.mcache + (size_t)row * a.mc_stride;
+        const int* skey = lofs >= 0 ? a.sp.key + lofs : reinterpret_cast<const int*>(slot + a.mc_list);
+        // (round 5: a lane's first entries loaded before the clear and the rest 2-4 at a time
+        // measured scircuit-like / cant-s1-like +1-2 % at 256 threads and 1024, cop20k-like -2..+4 %)
         clear_tiles(tm, E, H);
         if (MODE == NM_HASH && tm.rank() == 0) *counter = 0;
         tm.sync();
-        const unsigned long long* slot = lofs >= 0 ? a.sp.mask + lofs : a.mcache + (size_t)row * a.mc_stride;
-        const int* skey = lofs >= 0 ? a.sp.key + lofs : reinterpret_cast<const int*>(slot + a.mc_list);
         for (int r = tm.rank(); r < t; r += Team::size) {
             const unsigned long long m = ld_cache(&slot[r]);
             const int key = ld_cache(&skey[r]);
@@ -3851,7 +3876,7 @@ struct TinyArgs {
     double* sc_val;
     long long* tslot;
     long long sbase;
-    int blk0[TINY_SYM_NC + 1];  // slots: class c takes blocks [blk0[c], blk0[c+1]) (sized on the host)
+    int blk0[TINY_SYMX_NC + 1];  // slots: class c takes blocks [blk0[c], blk0[c+1]) (sized on the host)
 };
 
 template <int W, int K, bool NUMERIC>
@@ -4031,19 +4056,23 @@ __device__ __forceinline__ void tiny_sym_rows(TinyArgs a, int blk) {
     int c = blk / TINY_SYM_GRID, bid = blk % TINY_SYM_GRID, nb = TINY_SYM_GRID;
     if (a.nft) {  // numeric-first slots: the grid follows the bins' sizes, as numeric's does
         // (constant indices only: a dynamically indexed kernel argument goes to scratch)
-        static_assert(TINY_SYM_NC == 4, "class ranges below");
-        const int b1 = a.blk0[1], b2 = a.blk0[2], b3 = a.blk0[3], b4 = a.blk0[4];
-        c = (blk >= b1) + (blk >= b2) + (blk >= b3);
-        const int lo = c == 0 ? 0 : c == 1 ? b1 : c == 2 ? b2 : b3;
-        const int hi = c == 0 ? b1 : c == 1 ? b2 : c == 2 ? b3 : b4;
+        static_assert(TINY_SYM_NC == 4 && TINY_SYMX_NC == 5, "class ranges below");
+        const int b1 = a.blk0[1], b2 = a.blk0[2], b3 = a.blk0[3], b4 = a.blk0[4], b5 = a.blk0[5];
+        c = (blk >= b1) + (blk >= b2) + (blk >= b3) + (blk >= b4);
+        const int lo = c == 0 ? 0 : c == 1 ? b1 : c == 2 ? b2 : c == 3 ? b3 : b4;
+        const int hi = c == 0 ? b1 : c == 1 ? b2 : c == 2 ? b3 : c == 3 ? b4 : b5;
         bid = blk - lo;
         nb = hi - lo;
     }
     static_assert(TINY_NC == 6 && TINY_SYM_NC == 4 && tiny_ws(3) <= 32 && tiny_w(3) <= 32 && tiny_w(4) == 64 &&
-                      tiny_w(5) == 64,
+                      tiny_w(5) == 64 && tiny_ws(4) == 64,
                   "k_tiny_sym / launch_tiny_num instantiate the classes of tiny_class()");
     a.bin = SYM_TINY + c;
     a.list += (long long)c * a.M;
+    if (c == 4) {  // the scattered class counts only, in either mode
+        tiny_rows<tiny_ws(4), tiny_ks(4), false>(a, bid, nb);
+        return;
+    }
     if (!a.nft) {
         switch (c) {
         case 0: tiny_rows<tiny_ws(0), tiny_ks(0), false>(a, bid, TINY_SYM_GRID); break;
@@ -4200,8 +4229,8 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG, UU) hipLaunchKernelGGL((k_analyze<GG, UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr)
-#define MHS_ANALYZE_LANE(UU) hipLaunchKernelGGL((k_analyze_lane<UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr)
+#define MHS_ANALYZE(GG, UU) hipLaunchKernelGGL((k_analyze<GG, UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, w.tiny_num && MHS_SYM_SORT64)
+#define MHS_ANALYZE_LANE(UU) hipLaunchKernelGGL((k_analyze_lane<UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, w.tiny_num && MHS_SYM_SORT64)
     switch (G) {
     case 1:
         if (A.nnz < 4LL * A.M) MHS_ANALYZE_LANE(4);
@@ -4367,13 +4396,14 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
         t.sc_val = w.sc_val;
         t.tslot = w.tslot;
     }
-    int tiny_blocks = TINY_SYM_GRID * TINY_SYM_NC;
+    int tiny_blocks = TINY_SYM_GRID * (MHS_SYM_SORT64 ? TINY_SYMX_NC : TINY_SYM_NC);
     if (t.nft) {  // (the classes' sizes are on the device: grids for M rows each, as numeric's)
         for (int c = 0; c < TINY_SYM_NC; ++c) {
             const int per = 256 / tiny_w(c);
             t.blk0[c + 1] = t.blk0[c] + round8((M + per - 1) / per, 4096);
         }
-        tiny_blocks = t.blk0[TINY_SYM_NC];
+        t.blk0[TINY_SYMX_NC] = t.blk0[TINY_SYM_NC] + (MHS_SYM_SORT64 ? TINY_SYM_GRID : 0);  // class 4: a walk
+        tiny_blocks = t.blk0[TINY_SYMX_NC];
     }
     hipLaunchKernelGGL(k_sym_common<SYM_WAVE_BYTES>, dim3(wave_blocks + tiny_blocks), dim3(256),
                        WPB * SYM_WAVE_BYTES, s, a, t, wave_blocks);
@@ -4434,7 +4464,7 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
 #define MHS_SCAN(P)                                                                                                \
     hipLaunchKernelGGL(k_scan<P>, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop,  \
                        w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
-                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, w.gna, w.near_b ? w.bmeta : nullptr)
+                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, w.gna, w.near_b ? w.bmeta : nullptr, w.sym_bin)
     if (per == 4) MHS_SCAN(4);
     else MHS_SCAN(1);
 #undef MHS_SCAN

@@ -762,3 +762,29 @@ def test_numeric_first_without_probe(tool, auto, monkeypatch):
         assert (t2.stat("nft") > 0) == (auto != "0"), t2.stat("nft")
     finally:
         t2.close()
+
+
+@pytest.mark.parametrize("mode", ["nft", "plain", "notiny"])
+def test_symbolic_scattered_sort_class(tool, mode, monkeypatch):
+    """Round 5: rows of at most 512 products whose symbolic tables would not fit the small wave
+    bin (a hub column's B row beside short ones; web-graph rows) count by a 64-lane register sort
+    (symbolic bin 9) and k_scan sends them to numeric's 64-lane sort classes, since symbolic kept
+    no masks for them -- with numeric-first slots (nft), without (plain), and off with the numeric
+    tiny classes (notiny: those rows then count in tables and keep their masks)."""
+    if mode == "plain":
+        monkeypatch.setenv("MHS_NFT_AUTO_AVG", "0")
+    if mode == "notiny":
+        monkeypatch.setenv("MHS_NO_TINY_NUM", "1")
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        for name in ("scircuit", "webbase-1M"):
+            A = synth.SYNTH[name]()
+            t = check(t2, A, A)
+            if mode == "notiny":
+                assert t.sym_bins[9] == 0, t.sym_bins
+            else:
+                assert t.sym_bins[9] > 0, t.sym_bins
+                assert t.num_bins[12] + t.num_bins[13] >= t.sym_bins[9], t.num_bins
+            A.d_release_csr()
+    finally:
+        t2.close()
