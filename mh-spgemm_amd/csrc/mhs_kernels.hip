@@ -60,6 +60,15 @@
 #ifndef MHS_NUM_W16H_GRID
 #define MHS_NUM_W16H_GRID 2048  // block cap of the 10 KiB hash launch (4096: neutral at 16 KiB, profiles/r02za2_grid)
 #endif
+#ifndef MHS_SYM_WAVE_GRID
+#define MHS_SYM_WAVE_GRID 2048  // block cap of k_sym_common's wave rows (65536: cage15-like -3 %, cop20k-, webbase-, mac_econ-like +5 %)
+#endif
+#ifndef MHS_NUM_WSH_BIG
+#define MHS_NUM_WSH_BIG (1 << 21)  // small hash bins of at least this many rows: block cap MHS_NUM_WSH_BIG_GRID
+#endif
+#ifndef MHS_NUM_WSH_BIG_GRID
+#define MHS_NUM_WSH_BIG_GRID 65536  // (cage15-like -2.5 % over 16384; 65536 for every bin: offshore-, webbase-like +1.5 %)
+#endif
 #ifndef MHS_NUM_WSX_GRID
 #define MHS_NUM_WSX_GRID 16384  // ... of the small-row hash / direct launches (8192: cage15-like numeric +4.5 %, 4096: +13 %,
 #endif                         // cant-perturbed +5 %; the grouped launch: 8192 measured +1.4 % on cant-like)
@@ -3703,6 +3712,9 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
 // kernel that has its mode): the hash body's register sort would otherwise set the
 // register budget -- and the occupancy -- of the direct-mapped wave kernels too.
 enum NumModes : int { MODES_ALL = 0, MODES_NOHASH = 1, MODES_HASH = 2 };
+#ifndef MHS_GRP_MODES
+#define MHS_GRP_MODES MODES_ALL
+#endif
 
 // Row-level scalars are made provably wave-uniform (readfirstlane) so that the
 // mode dispatch and every per-row loop bound compile to scalar control flow.
@@ -3754,7 +3766,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     auto one = [&](int li) {
         const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
         if constexpr (GROUPED)  // a group head: R rows of one pattern
-            num_row<WaveTeam, false, true, MODES_ALL, O32>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
+            num_row<WaveTeam, false, true, MHS_GRP_MODES, O32>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
                                                          __builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_RMASK);
         else
             num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH, O32>(tm, a, row, reg + WAVE_HDR,
@@ -3769,6 +3781,8 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     // pdb1HYS-like neutral; the whole bin from the cursor (2 rows a take): wb-edu -12 %,
     // webbase -10 %, but cage15 +3.5 %; the direct / grouped 16 KiB bins guided: pdb1HYS +10 %.
     constexpr bool guided = BYTES == NUM_W16_BYTES && HASH;
+    // (round 5: the small hash bin from the XCD groups' cursors, 2-8 rows a take, measured
+    // cage15-like +3 %, cop20k-like +16 %, offshore-like +14 %)
     if (guided && a.qall) {
         WaveQueue q(a.cursor, a.count, 1);
         for (int li; q.next(li);) one(li);
@@ -4374,7 +4388,7 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
     if (M <= 0) return;
     SymArgs a = sym_args(A, w, M, N, Cptr);
     a.bin = SYM_WAVE;
-    const int wave_blocks = round8((M + WPB - 1) / WPB, 2048);
+    const int wave_blocks = round8((M + WPB - 1) / WPB, MHS_SYM_WAVE_GRID);
     TinyArgs t{};
     t.M = M;
     t.Aptr = A.ptr;
@@ -4726,7 +4740,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     if (h.num_count[NUM_WSH] > 0) {
         const NumArgs x = wave_args(NUM_WSH);
-        const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WSX_GRID));
+        const dim3 grid(round8((x.count + WPB - 1) / WPB, x.count >= MHS_NUM_WSH_BIG ? MHS_NUM_WSH_BIG_GRID : MHS_NUM_WSX_GRID));
         add([=](hipStream_t s) {
             if (o32) hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
             else hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
