@@ -37,8 +37,9 @@ __device__ __forceinline__ void st(v4i* p, v4i v) {
 
 // Block b owns [b*per, (b+1)*per) (SLAB) or every grid-stride U-group (!SLAB); a lane issues U
 // loads, then U stores.
-template <bool NT, int U, bool SLAB>
+template <bool NT, int U, bool SLAB, int STNT = -1>  // STNT: stores' nontemporal flag (-1: as NT)
 __global__ __launch_bounds__(HBM_T) void k_hbm_copy(const v4i* __restrict__ src, v4i* __restrict__ dst, long long n) {
+    constexpr bool SNT = STNT < 0 ? NT : STNT != 0;
     long long i, end, stride;
     if (SLAB) {
         const long long per = (n + gridDim.x - 1) / gridDim.x;
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(HBM_T) void k_hbm_copy(const v4i* __restrict__ src,
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = ld<NT>(src + i + u * stride);
 #pragma unroll
-        for (int u = 0; u < U; ++u) st<NT>(dst + i + u * stride, v[u]);
+        for (int u = 0; u < U; ++u) st<SNT>(dst + i + u * stride, v[u]);
     }
     for (; i < end; i += stride) dst[i] = src[i];
 }
@@ -85,16 +86,25 @@ __global__ __launch_bounds__(HBM_T) void k_hbm_read(const v4i* __restrict__ src,
     if (acc == 0x7FFFFFFF) out[blockIdx.x] = acc;  // (data-dependent: the loads cannot be dropped)
 }
 
-template <bool NT, int U = 1>
+template <bool NT, int U = 1, bool SLAB = false>
 __global__ __launch_bounds__(HBM_T) void k_hbm_write(v4i* __restrict__ dst, long long n, int seed) {
-    const long long stride = (long long)gridDim.x * HBM_T;
+    long long i, end, stride;
+    if (SLAB) {
+        const long long per = (n + gridDim.x - 1) / gridDim.x;
+        i = (long long)blockIdx.x * per + threadIdx.x;
+        end = min(n, (long long)(blockIdx.x + 1) * per);
+        stride = HBM_T;
+    } else {
+        i = (long long)blockIdx.x * HBM_T + threadIdx.x;
+        end = n;
+        stride = (long long)gridDim.x * HBM_T;
+    }
     const v4i v = v4i{seed, seed + 1, seed + 2, seed + 3};
-    long long i = (long long)blockIdx.x * HBM_T + threadIdx.x;
-    for (; i + (U - 1) * stride < n; i += U * stride) {
+    for (; i + (U - 1) * stride < end; i += U * stride) {
 #pragma unroll
         for (int u = 0; u < U; ++u) st<NT>(dst + i + u * stride, v);
     }
-    for (; i < n; i += stride) st<NT>(dst + i, v);
+    for (; i < end; i += stride) st<NT>(dst + i, v);
 }
 
 struct Shape {
@@ -103,17 +113,17 @@ struct Shape {
     void (*launch)(int grid, hipStream_t s, v4i* a, v4i* b, long long n, int* sink);
 };
 
-template <bool NT, int U, bool SLAB>
+template <bool NT, int U, bool SLAB, int STNT = -1>
 void l_copy(int g, hipStream_t s, v4i* a, v4i* b, long long n, int*) {
-    hipLaunchKernelGGL((k_hbm_copy<NT, U, SLAB>), dim3(g), dim3(HBM_T), 0, s, a, b, n);
+    hipLaunchKernelGGL((k_hbm_copy<NT, U, SLAB, STNT>), dim3(g), dim3(HBM_T), 0, s, a, b, n);
 }
 template <int U, bool SLAB>
 void l_read(int g, hipStream_t s, v4i* a, v4i*, long long n, int* sink) {
     hipLaunchKernelGGL((k_hbm_read<U, SLAB>), dim3(g), dim3(HBM_T), 0, s, a, n, sink);
 }
-template <bool NT, int U = 1>
+template <bool NT, int U = 1, bool SLAB = false>
 void l_write(int g, hipStream_t s, v4i*, v4i* b, long long n, int*) {
-    hipLaunchKernelGGL((k_hbm_write<NT, U>), dim3(g), dim3(HBM_T), 0, s, b, n, 7);
+    hipLaunchKernelGGL((k_hbm_write<NT, U, SLAB>), dim3(g), dim3(HBM_T), 0, s, b, n, 7);
 }
 // the runtime's own blit kernels, for comparison (labelled in the shape list)
 void l_blit_copy(int, hipStream_t s, v4i* a, v4i* b, long long n, int*) {
@@ -130,6 +140,13 @@ const Shape kShapes[] = {
     {2, 16, l_write<true>},           {2, 16, l_write<false>},          {2, 4, l_write<true>},
     {2, 32, l_write<false>},          {2, 8, l_write<true, 4>},         {2, 2, l_write<true, 4>},
     {2, 4, l_write<false, 4>},        {0, 1, l_blit_copy},              {2, 1, l_blit_fill},
+    // slabs for the writes and fewer, longer-lived blocks for the copies (round 5: the write
+    // side held the copy at ~5.5 TB/s where the runtime's fill reached 6.5)
+    {2, 1, l_write<true, 4, true>},   {2, 2, l_write<true, 4, true>},   {2, 4, l_write<false, 4, true>},
+    {2, 8, l_write<true, 8, true>},   {0, 1, l_copy<true, 8, true>},    {0, 2, l_copy<true, 8, true>},
+    {0, 2, l_copy<false, 8, true>},   {0, 1, l_copy<true, 16, true>},   {0, 4, l_copy<false, 16, true>},
+    {0, 16, l_copy<true, 4, true, 0>}, {0, 8, l_copy<true, 4, true, 0>}, {0, 4, l_copy<true, 8, true, 0>},
+    {0, 16, l_copy<false, 4, true, 1>}, {0, 32, l_copy<true, 2, true>}, {0, 16, l_copy<true, 2, true>},
 };
 
 }  // namespace
