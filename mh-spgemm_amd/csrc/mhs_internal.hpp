@@ -28,9 +28,7 @@ constexpr int TILE_BITS = 64;
 constexpr int NBINS = 16;  // capacity of the per-bin counters
 constexpr int WPB = 4;          // waves per block in the wave-per-row kernels
 constexpr int LDS_MAX_C = 163840;  // gfx950: 160 KiB per workgroup (probed on the box)
-#ifndef MHS_SCAN_ITEMS
-#define MHS_SCAN_ITEMS 1024
-#endif
+constexpr int MHS_SCAN_ITEMS = 1024;
 constexpr int SCAN_ITEMS = MHS_SCAN_ITEMS;  // rows per block (of 1024 threads) in the row_ptr scan and the bin lists
 // Row cursors of the dynamically scheduled bin walks: a launch slot (numeric bin b: b,
 // symbolic bin b: NUM_NB + b) has one cursor per XCD group, 64 bytes apart.  They live after
@@ -74,12 +72,8 @@ constexpr int TINY_SYM_NC = 4;
 // the small wave table cannot hold (k_analyze's sym_tiny_class: a hub column's B row in the
 // row, web-graph rows), which otherwise count in 10 KiB waves or block tables
 constexpr int TINY_SYMX_NC = 5;
-#ifndef MHS_SYM_SORT64
-#define MHS_SYM_SORT64 1
-#endif
-#ifndef MHS_TINY_NUM_SMALL
-#define MHS_TINY_NUM_SMALL 4
-#endif
+constexpr int MHS_SYM_SORT64 = 1;
+constexpr int MHS_TINY_NUM_SMALL = 4;
 constexpr int TINY_NUM_SMALL = MHS_TINY_NUM_SMALL;  // numeric classes >= this only replace big-table rows
 __host__ __device__ inline int tiny_class(int flop, int nA, int nc = TINY_NC) {
     if (flop <= 0) return -1;

@@ -36,84 +36,36 @@
 #ifndef MHS_ROW_STAMPS
 #define MHS_ROW_STAMPS 0  // 1: tools/diag/stamps*.py builds -- per-row, per-phase s_memtime cycles
 #endif
-#ifndef MHS_RUN_MAX
-#define MHS_RUN_MAX 3  // longest run a value walk merges into one accumulate (1..4)
-#endif
-#ifndef MHS_RUN_UNROLL
-#define MHS_RUN_UNROLL 2  // B entries per lane issued together in a run walk (registers: occupancy)
-#endif
-#ifndef MHS_TILE_UNROLL
-#define MHS_TILE_UNROLL 2  // tiles per lane issued together in a tile walk
-#endif
-#ifndef MHS_UNROLL
-#define MHS_UNROLL 4  // B entries per lane issued together in the product walk
-#endif
-#ifndef MHS_UNROLL_BLOCK
-#define MHS_UNROLL_BLOCK 8  // ... in the block kernels (measured: S1-like rows -9%; the wave kernels keep 4)
-#endif
-#ifndef MHS_NUM_WS_GRID
-#define MHS_NUM_WS_GRID 4096  // block cap of the small-row grouped numeric launch
-#endif
-#ifndef MHS_TINY64_GRID
-#define MHS_TINY64_GRID 4096  // block cap of the 64-lane tiny numeric launches (8192: wb-edu-like +6 %)
-#endif
-#ifndef MHS_NUM_W16H_GRID
-#define MHS_NUM_W16H_GRID 2048  // block cap of the 10 KiB hash launch (4096: neutral at 16 KiB, profiles/r02za2_grid)
-#endif
-#ifndef MHS_SYM_WAVE_GRID
-#define MHS_SYM_WAVE_GRID 2048  // block cap of k_sym_common's wave rows (65536: cage15-like -3 %, cop20k-, webbase-, mac_econ-like +5 %)
-#endif
-#ifndef MHS_NUM_WSH_BIG
-#define MHS_NUM_WSH_BIG (1 << 21)  // small hash bins of at least this many rows: block cap MHS_NUM_WSH_BIG_GRID
-#endif
-#ifndef MHS_NUM_WSH_BIG_GRID
-#define MHS_NUM_WSH_BIG_GRID 65536  // (cage15-like -2.5 % over 16384; 65536 for every bin: offshore-, webbase-like +1.5 %)
-#endif
-#ifndef MHS_NUM_WSX_GRID
-#define MHS_NUM_WSX_GRID 16384  // ... of the small-row hash / direct launches (8192: cage15-like numeric +4.5 %, 4096: +13 %,
-#endif                         // cant-perturbed +5 %; the grouped launch: 8192 measured +1.4 % on cant-like)
-#ifndef MHS_VAL_GMIN
-#define MHS_VAL_GMIN 4  // narrowest lane group of a value walk
-#endif
-#ifndef MHS_TILE_GMIN
-#define MHS_TILE_GMIN 4  // narrowest lane group of a tile walk
-#endif
-#ifndef MHS_RUN_GMIN
-#define MHS_RUN_GMIN 8  // narrowest lane group of a chunk with merged runs (32 before: see DESIGN §8)
-#endif
-#ifndef MHS_MASK_GMAX
-#define MHS_MASK_GMAX 64
-#endif
-#ifndef MHS_AN_GMAX
-#define MHS_AN_GMAX 8  // k_analyze: 8 lanes per row (several rows per wave overlap their load chains)
-#endif
-#ifndef MHS_GRP_UNROLL
-#define MHS_GRP_UNROLL 3  // entries per lane issued together in a row-group walk
-#endif
+constexpr int MHS_RUN_MAX = 3;  // longest run a value walk merges into one accumulate (1..4)
+constexpr int MHS_RUN_UNROLL = 2;  // B entries per lane issued together in a run walk (registers: occupancy)
+constexpr int MHS_TILE_UNROLL = 2;  // tiles per lane issued together in a tile walk
+constexpr int MHS_UNROLL = 4;  // B entries per lane issued together in the product walk
+constexpr int MHS_UNROLL_BLOCK = 8;  // ... in the block kernels (measured: S1-like rows -9%; the wave kernels keep 4)
+constexpr int MHS_NUM_WS_GRID = 4096;  // block cap of the small-row grouped numeric launch
+constexpr int MHS_TINY64_GRID = 4096;  // block cap of the 64-lane tiny numeric launches (8192: wb-edu-like +6 %)
+constexpr int MHS_NUM_W16H_GRID = 2048;  // block cap of the 10 KiB hash launch (4096: neutral at 16 KiB, profiles/r02za2_grid)
+constexpr int MHS_SYM_WAVE_GRID = 2048;  // block cap of k_sym_common's wave rows (65536: cage15-like -3 %, cop20k-, webbase-, mac_econ-like +5 %)
+constexpr int MHS_NUM_WSH_BIG = (1 << 21);  // small hash bins of at least this many rows: block cap MHS_NUM_WSH_BIG_GRID
+constexpr int MHS_NUM_WSH_BIG_GRID = 65536;  // (cage15-like -2.5 % over 16384; 65536 for every bin: offshore-, webbase-like +1.5 %)
+constexpr int MHS_NUM_WSX_GRID = 16384;  // ... of the small-row hash / direct launches (8192: cage15-like numeric +4.5 %, 4096: +13 %,
+                                         // cant-perturbed +5 %; the grouped launch: 8192 measured +1.4 % on cant-like)
+constexpr int MHS_VAL_GMIN = 4;  // narrowest lane group of a value walk
+constexpr int MHS_TILE_GMIN = 4;  // narrowest lane group of a tile walk
+constexpr int MHS_RUN_GMIN = 8;  // narrowest lane group of a chunk with merged runs (32 before: see DESIGN §8)
+constexpr int MHS_MASK_GMAX = 64;
+constexpr int MHS_AN_GMAX = 8;  // k_analyze: 8 lanes per row (several rows per wave overlap their load chains)
+constexpr int MHS_GRP_UNROLL = 3;  // entries per lane issued together in a row-group walk
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice).  The wave kernels are
 // bound by per-row latency chains, so waves in flight matter more than a few spills.
-#ifndef MHS_WPE_HASH
-#define MHS_WPE_HASH 8  // measured: cop20k-like numeric -18%, cage15-like -16% (vs the compiler's 6)
-#endif
-#ifndef MHS_SYM_B256_GRID
-#define MHS_SYM_B256_GRID 1024  // block cap of the persistent 256-thread symbolic bin launch
-#endif
-#ifndef MHS_WPE_HASH16
-#define MHS_WPE_HASH16 4  // the 10 KiB hash bin: LDS allows 4 waves per SIMD (an 8-wave register target spilled 34 VGPRs for nothing)
-#endif
-#ifndef MHS_WPE_GRP
-#define MHS_WPE_GRP 0  // occupancy floor of the generic / grouped wave numeric kernel (0: compiler's choice)
-#endif
-#ifndef MHS_WPE_DIRECT
-#define MHS_WPE_DIRECT 0
-#endif
-#ifndef MHS_WPE_TINY
-#define MHS_WPE_TINY 0
-#endif
+constexpr int MHS_WPE_HASH = 8;  // measured: cop20k-like numeric -18%, cage15-like -16% (vs the compiler's 6)
+constexpr int MHS_SYM_B256_GRID = 1024;  // block cap of the persistent 256-thread symbolic bin launch
+constexpr int MHS_WPE_HASH16 = 4;  // the 10 KiB hash bin: LDS allows 4 waves per SIMD (an 8-wave register target spilled 34 VGPRs for nothing)
+// (the generic / grouped wave numeric kernel: no occupancy floor -- the compiler's choice; a
+// 5-wave floor at 96 VGPRs measured slower)
+constexpr int MHS_WPE_DIRECT = 0;
+constexpr int MHS_WPE_TINY = 0;
 #define MHS_WPE_ATTR(n) __attribute__((amdgpu_waves_per_eu((n) > 0 ? (n) : 1)))
-#ifndef MHS_WPE_SYM
-#define MHS_WPE_SYM 8  // symbolic wave + tiny kernels: cant-like -12%, cop20k-like -22%
-#endif
+constexpr int MHS_WPE_SYM = 8;  // symbolic wave + tiny kernels: cant-like -12%, cop20k-like -22%
 #if MHS_ROW_STAMPS  // diagnostic build: per-row, per-phase s_memtime cycles (plain stores)
 __device__ unsigned long long* g_rowdiag;  // [M][8]
 #define MHS_STAMP0() unsigned long long tp_ = __builtin_amdgcn_s_memtime()
@@ -191,15 +143,9 @@ namespace mhs {
 
 // ------------------------------------------------------------------ helpers ---
 
-#ifndef MHS_TINY_DUP
-#define MHS_TINY_DUP 2  // ... and at most this many products a C column
-#endif
-#ifndef MHS_TINY_SPARSE_PCT
-#define MHS_TINY_SPARSE_PCT 50  // class-4 rows with tiles >= this % of their C columns go to the sort class (0: off)
-#endif
-#ifndef MHS_LANE_AVG
-#define MHS_LANE_AVG 9  // k_mask_b / k_analyze: a lane per row below this many entries a row on average (0: off)
-#endif
+constexpr int MHS_TINY_DUP = 2;  // ... and at most this many products a C column
+constexpr int MHS_TINY_SPARSE_PCT = 50;  // class-4 rows with tiles >= this % of their C columns go to the sort class (0: off)
+constexpr int MHS_LANE_AVG = 9;  // k_mask_b / k_analyze: a lane per row below this many entries a row on average (0: off)
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Ordering point for LDS traffic between lanes of ONE wave: a wave's LDS
@@ -514,19 +460,11 @@ struct RowWalk {
     }
 };
 
-#ifndef MHS_GRP_CHUNK
-#define MHS_GRP_CHUNK 63  // A entries staged per chunk in the grouped walk (<= 64)
-#endif
+constexpr int MHS_GRP_CHUNK = 63;  // A entries staged per chunk in the grouped walk (<= 64)
 static_assert(MHS_GRP_CHUNK >= 1 && MHS_GRP_CHUNK <= 64, "a chunk is one entry per lane");
-#ifndef MHS_SYMWM_DYN_MAX
-#define MHS_SYMWM_DYN_MAX 32768  // k_sym_rare's 10 KiB wave rows from the cursors up to this many rows
-#endif
-#ifndef MHS_DYN16_MAX
-#define MHS_DYN16_MAX 32768  // hash 10 KiB bins of at most this many rows: all rows from the cursor
-#endif
-#ifndef MHS_GUIDED_STATIC
-#define MHS_GUIDED_STATIC 4  // eighths of an XCD group's rows walked statically before the cursor
-#endif
+constexpr int MHS_SYMWM_DYN_MAX = 32768;  // k_sym_rare's 10 KiB wave rows from the cursors up to this many rows
+constexpr int MHS_DYN16_MAX = 32768;  // hash 10 KiB bins of at most this many rows: all rows from the cursor
+constexpr int MHS_GUIDED_STATIC = 4;  // eighths of an XCD group's rows walked statically before the cursor
 // Dynamic XCD-grouped walk: group g = blockIdx % 8 (an XCD under round-robin dispatch) owns
 // the g-th eighth of the list; its waves take CH consecutive entries at a time from the
 // group's cursor, in list order.  The rows in flight on an XCD stay one compact window
@@ -1813,14 +1751,10 @@ __device__ __forceinline__ void for_products(const BlockTeam<T, GM>&, int a0, in
 // (row stamps: ~170 k cycles per walk).  The group width counts the chunk's longest segment too
 // (a hub column's long B row among short ones).  (For the 256-thread kernels the pieces measured
 // slower: scircuit-like +3 %, cant-s1-like +4 %.)
-#ifndef MHS_PIECES
-#define MHS_PIECES 1
-#endif
+constexpr int MHS_PIECES = 1;
 // (round 5: single wave rows' first A chunk loaded before the tile table, as row groups do --
 // cage15-like +5 %, offshore-like +10 %, cop20k-like +4 %: the 5 KiB hash kernel spills at 8 waves)
-#ifndef MHS_PIECE_UNROLL
-#define MHS_PIECE_UNROLL 2  // B entries per lane issued together in a piece's value walk (registers)
-#endif
+constexpr int MHS_PIECE_UNROLL = 2;  // B entries per lane issued together in a piece's value walk (registers)
 __device__ __forceinline__ int chunk_group_mx(int nh, int avg, int mx, int U, int gmin) {
     int best = gmin, bc = INT_MAX;
     for (int g = gmin; g <= 64; g <<= 1) {
@@ -2534,9 +2468,7 @@ struct NearArgs {
     long long vcheck_n;
     int* nonfinite;  // Stats::nonfinite
 };
-#ifndef MHS_NEAR_GRID
-#define MHS_NEAR_GRID 2048  // k_near's block cap
-#endif
+constexpr int MHS_NEAR_GRID = 2048;  // k_near's block cap
 constexpr int NEAR_PER = 4;  // A entries a lane holds: a group's R rows of at most 256 entries
 constexpr int NEAR_LDS = NEAR_WORDS * 12 + RG_MAX * NEAR_UMAX * 8;  // a wave's bitmap, word prefixes, values
 static_assert(16 * NEAR_LDS <= LDS_MAX_C - 1024, "k_sym_rare's 16 waves hold their near-group regions");
@@ -3712,9 +3644,6 @@ __device__ void num_row_bitmap(const BlockTeam<T, false>& tm, const NumArgs& a, 
 // kernel that has its mode): the hash body's register sort would otherwise set the
 // register budget -- and the occupancy -- of the direct-mapped wave kernels too.
 enum NumModes : int { MODES_ALL = 0, MODES_NOHASH = 1, MODES_HASH = 2 };
-#ifndef MHS_GRP_MODES
-#define MHS_GRP_MODES MODES_ALL
-#endif
 
 // Row-level scalars are made provably wave-uniform (readfirstlane) so that the
 // mode dispatch and every per-row loop bound compile to scalar control flow.
@@ -3766,7 +3695,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     auto one = [&](int li) {
         const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
         if constexpr (GROUPED)  // a group head: R rows of one pattern
-            num_row<WaveTeam, false, true, MHS_GRP_MODES, O32>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
+            num_row<WaveTeam, false, true, MODES_ALL, O32>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
                                                          __builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_RMASK);
         else
             num_row<WaveTeam, false, false, HASH ? MODES_HASH : MODES_NOHASH, O32>(tm, a, row, reg + WAVE_HDR,
@@ -3806,11 +3735,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
 }
 
 template <int BYTES, bool GROUPED = false, bool HASH = false, bool O32 = false>
-#if MHS_WPE_GRP > 0
-__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_GRP) void k_num_wave(NumArgs a) {
-#else
 __global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
-#endif
     num_wave_rows<BYTES, GROUPED, HASH, O32>(a);
 }
 template <int BYTES, bool O32 = false>
@@ -4167,14 +4092,10 @@ __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_common(Sy
 // matrices -- a quarter of the blocks, so a quarter of the per-(block, bin) cursor atomics
 // (tiny-row matrices of millions of rows were bound by them) -- 1024 below, where fewer
 // blocks would leave the chip idle (measured: cant-like -6% at 4096).
-#ifndef MHS_SCAN_BIG_M
-#define MHS_SCAN_BIG_M (1 << 19)
-#endif
+constexpr int MHS_SCAN_BIG_M = (1 << 19);
 static int scan_per(int M) { return M >= MHS_SCAN_BIG_M ? 4 : 1; }
 
-#ifndef MHS_ROW_GMIN
-#define MHS_ROW_GMIN 4  // narrowest lane group per row in k_mask_b / k_analyze (tiny rows: 16 per wave)
-#endif
+constexpr int MHS_ROW_GMIN = 4;  // narrowest lane group per row in k_mask_b / k_analyze (tiny rows: 16 per wave)
 static int pick_group(long long nnz, int rows, int gmax = 64) {
     const long long avg = rows > 0 ? (nnz + rows - 1) / rows : 1;
     int g = MHS_ROW_GMIN;
