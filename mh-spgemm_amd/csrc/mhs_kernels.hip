@@ -44,6 +44,7 @@ constexpr int MHS_UNROLL_BLOCK = 8;  // ... in the block kernels (measured: S1-l
 constexpr int MHS_NUM_WS_GRID = 4096;  // block cap of the small-row grouped numeric launch
 constexpr int MHS_TINY64_GRID = 4096;  // block cap of the 64-lane tiny numeric launches (8192: wb-edu-like +6 %)
 constexpr int MHS_NUM_W16H_GRID = 2048;  // block cap of the 10 KiB hash launch (4096: neutral at 16 KiB, profiles/r02za2_grid)
+constexpr int MHS_TINY_PF = 1;  // tiny teams load their next row a round ahead (GAP-road-like -3 %, mac_econ-, scircuit-like -1 %)
 constexpr int MHS_SYM_WAVE_GRID = 2048;  // block cap of k_sym_common's wave rows (65536: cage15-like -3 %, cop20k-, webbase-, mac_econ-like +5 %)
 constexpr int MHS_NUM_WSH_BIG = (1 << 21);  // small hash bins of at least this many rows: block cap MHS_NUM_WSH_BIG_GRID
 constexpr int MHS_NUM_WSH_BIG_GRID = 65536;  // (cage15-like -2.5 % over 16384; 65536 for every bin: offshore-, webbase-like +1.5 %)
@@ -3826,8 +3827,16 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
     const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W), bid, nb);
     extern __shared__ __attribute__((aligned(16))) char tiny_smem[];
     double* vstage = (double*)tiny_smem + (size_t)(threadIdx.x / W) * (W * K);  // numeric: W*K doubles per team
-    // the wave iterates while any of its teams has a row (shuffles need every lane)
-    for (int it = rw.first; __ballot(it < rw.end) != 0; it += rw.stride) {
+    // the wave iterates while any of its teams has a row (shuffles need every lane).  A team's
+    // next row (list entry, then its A pointers) is loaded a round ahead, under this row's chain
+    int it = rw.first;
+    int nrow = 0, na0 = 0, na1 = 0;
+    if (MHS_TINY_PF && it < rw.end) {
+        nrow = a.list[it];
+        na0 = a.Aptr[nrow];
+        na1 = a.Aptr[nrow + 1];
+    }
+    for (; __ballot(it < rw.end) != 0; it += rw.stride) {
         // the lane's team masks, rebuilt every row from an opaque lane id: hoisted, they stayed
         // live across the fused kernels' class dispatch and went to scratch (64-VGPR budget)
         int lane = lane_id();
@@ -3837,8 +3846,11 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
         const unsigned long long tmask = W == 64 ? ~0ull : (((1ull << (W & 63)) - 1) << tb);
         const unsigned long long below = tmask & (lane == 0 ? 0ull : (~0ull >> (64 - lane)));
         const bool live = it < rw.end;
-        const int row = live ? a.list[it] : 0;
-        const int a0 = live ? a.Aptr[row] : 0, nA = live ? a.Aptr[row + 1] - a0 : 0;
+        const int row = MHS_TINY_PF ? nrow : live ? a.list[it] : 0;
+        const int a0 = MHS_TINY_PF ? na0 : live ? a.Aptr[row] : 0;
+        const int nA = !live ? 0 : MHS_TINY_PF ? na1 - na0 : a.Aptr[row + 1] - a0;
+        const bool ln = it + rw.stride < rw.end;
+        if (MHS_TINY_PF) nrow = ln ? a.list[it + rw.stride] : 0;
         long long c0 = (NUMERIC && live && !slots) ? a.Cptr[row] : 0;  // issued early: off the tail's chain
         const int cb = (NUMERIC && live) ? (a.rlo[row] << TILE_SHIFT) : 0;  // key origin (23-bit offsets)
         int st = 0, len = 0;
@@ -3880,6 +3892,10 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
         for (int i = 0; i < K; ++i) {
             bc[i] = a.Bcol[q[i]];
             if (NUMERIC) bv[i] = a.Bval[q[i]];
+        }
+        if (MHS_TINY_PF) {  // (after this row's B loads: the next row's pointers wait on its list entry)
+            na0 = ln ? a.Aptr[nrow] : 0;
+            na1 = ln ? a.Aptr[nrow + 1] : 0;
         }
 #pragma unroll
         for (int i = 0; i < K; ++i) {
