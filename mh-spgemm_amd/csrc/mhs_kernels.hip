@@ -44,6 +44,10 @@ constexpr int MHS_UNROLL_BLOCK = 8;  // ... in the block kernels (measured: S1-l
 constexpr int MHS_NUM_WS_GRID = 4096;  // block cap of the small-row grouped numeric launch
 constexpr int MHS_TINY64_GRID = 4096;  // block cap of the 64-lane tiny numeric launches (8192: wb-edu-like +6 %)
 constexpr int MHS_NUM_W16H_GRID = 2048;  // block cap of the 10 KiB hash launch (4096: neutral at 16 KiB, profiles/r02za2_grid)
+// block cap of each numeric-first symbolic tiny class: 4096, 16384 from 4 M rows (r05ab17/18:
+// delaunay-like 10.26 -> 9.70 ms, GAP-road-like 4.53 -> 4.43 at 16384, but mac_econ-, scircuit-like
+// +5-6 %; 512-2048 slower on every huge matrix, delaunay-like up to 19 ms)
+constexpr int MHS_NFT_GRID = 4096, MHS_NFT_GRID_BIG = 16384, MHS_NFT_BIG_M = 1 << 22;
 constexpr int MHS_TINY_PF = 1;  // tiny teams load their next row a round ahead (GAP-road-like -3 %, mac_econ-, scircuit-like -1 %)
 constexpr int MHS_SYM_WAVE_GRID = 2048;  // block cap of k_sym_common's wave rows (65536: cage15-like -3 %, cop20k-, webbase-, mac_econ-like +5 %)
 constexpr int MHS_NUM_WSH_BIG = (1 << 21);  // small hash bins of at least this many rows: block cap MHS_NUM_WSH_BIG_GRID
@@ -4351,7 +4355,7 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
     if (t.nft) {  // (the classes' sizes are on the device: grids for M rows each, as numeric's)
         for (int c = 0; c < TINY_SYM_NC; ++c) {
             const int per = 256 / tiny_w(c);
-            t.blk0[c + 1] = t.blk0[c] + round8((M + per - 1) / per, 4096);
+            t.blk0[c + 1] = t.blk0[c] + round8((M + per - 1) / per, M >= MHS_NFT_BIG_M ? MHS_NFT_GRID_BIG : MHS_NFT_GRID);
         }
         t.blk0[TINY_SYMX_NC] = t.blk0[TINY_SYM_NC] + (MHS_SYM_SORT64 ? TINY_SYM_GRID : 0);  // class 4: a walk
         tiny_blocks = t.blk0[TINY_SYMX_NC];
