@@ -47,6 +47,7 @@ constexpr int MHS_NUM_W16H_GRID = 2048;  // block cap of the 10 KiB hash launch 
 // block cap of each numeric-first symbolic tiny class: 4096, 16384 from 4 M rows (r05ab17/18:
 // delaunay-like 10.26 -> 9.70 ms, GAP-road-like 4.53 -> 4.43 at 16384, but mac_econ-, scircuit-like
 // +5-6 %; 512-2048 slower on every huge matrix, delaunay-like up to 19 ms)
+constexpr int MHS_COPY_CAP_BIG = 65536;  // the slot copy's block cap from 4 M rows (16384 below; delaunay-like -1 %, r05ab19)
 constexpr int MHS_NFT_GRID = 4096, MHS_NFT_GRID_BIG = 16384, MHS_NFT_BIG_M = 1 << 22;
 constexpr int MHS_TINY_PF = 1;  // tiny teams load their next row a round ahead (GAP-road-like -3 %, mac_econ-, scircuit-like -1 %)
 constexpr int MHS_SYM_WAVE_GRID = 2048;  // block cap of k_sym_common's wave rows (65536: cage15-like -3 %, cop20k-, webbase-, mac_econ-like +5 %)
@@ -4622,7 +4623,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             const CopyArgs ca{w.bin_list, A.M, Cptr, w.tslot, w.sc_col, w.sc_val, Ccol, Cval};
             // lanes per row by the median row's class
             const int Lw = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
-            const dim3 grid(round8((A.M + 256 / Lw - 1) / (256 / Lw), 16384));
+            const dim3 grid(round8((A.M + 256 / Lw - 1) / (256 / Lw), A.M >= MHS_NFT_BIG_M ? MHS_COPY_CAP_BIG : 16384));
             add([=](hipStream_t s) {
                 if (Lw == 4) hipLaunchKernelGGL(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
                 else if (Lw == 8) hipLaunchKernelGGL(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
