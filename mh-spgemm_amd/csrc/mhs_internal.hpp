@@ -72,7 +72,7 @@ constexpr int TINY_SYM_NC = 4;
 // the small wave table cannot hold (k_analyze's sym_tiny_class: a hub column's B row in the
 // row, web-graph rows), which otherwise count in 10 KiB waves or block tables
 constexpr int TINY_SYMX_NC = 5;
-constexpr int MHS_SYM_SORT64 = 1;
+constexpr int MHS_SYM_SORT64 = 1;  // symbolic class 4 on (k_analyze, k_sym_common, k_scan)
 constexpr int MHS_TINY_NUM_SMALL = 4;
 constexpr int TINY_NUM_SMALL = MHS_TINY_NUM_SMALL;  // numeric classes >= this only replace big-table rows
 __host__ __device__ inline int tiny_class(int flop, int nA, int nc = TINY_NC) {
