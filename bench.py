@@ -10,7 +10,10 @@ resident A -> device-resident sorted C (mask formation, symbolic, numeric, C
 allocation included: the t_e2e of BASELINE.md §2), C handed back to the
 context's output pool after the step.
 
-N = 1: one process.  N > 1 (torchrun, one rank per GPU, RCCL): rows of A are
+N = 1: one process.  N > 1: one rank per GPU over RCCL -- under torchrun (WORLD_SIZE set),
+or, run bare as `python bench.py --gpus N`, bench.py starts the N ranks itself (child
+processes, before any GPU call in the parent; --gpus above the visible GPU count is an
+error, never a 1-GPU fallback).  Rows of A are
 partitioned by flop, each rank starts with its row block of A (= of B); the
 exchange plan is built once (mhspgemm.distributed.ShardPlan, outside the timed
 steps) and a step is the exchange of B's rows over xGMI (--exchange halo: the
@@ -147,6 +150,56 @@ def cpu_baseline(A, budget_s: float = 12.0):
     return float(np.median(times)), threads, len(times), t1[0]
 
 
+def check_gpus(n: int, backend: str, ndev: int) -> None:
+    """--gpus N must name GPUs that exist (a gloo rehearsal may put every rank on one GPU)."""
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}: needs at least one GPU")
+    if backend != "gloo" and n > ndev:
+        raise SystemExit(f"bench.py: --gpus {n} but only {ndev} GPU(s) visible (no silent 1-GPU fallback)")
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(cmd, n: int, poll_s: float = 0.2) -> int:
+    """Start `cmd` as n child processes, one per rank (RANK = LOCAL_RANK = r, WORLD_SIZE = n,
+    rendezvous on 127.0.0.1), wait for all of them and return the first non-zero exit code
+    (the other ranks are then terminated: a dead rank would leave them in a collective).
+    The parent never touches the GPU; rank 0's stdout (the JSON line) is inherited."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, MHS_BENCH_LAUNCH="bench.py spawned its ranks", RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen(list(cmd), env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    for q in live:
+                        q.terminate()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,20 +217,28 @@ def main():
     ap.add_argument("--no-configs", action="store_true", help="N=1: skip the configs block")
     args = ap.parse_args()
 
-    import torch
+    # MHS_BENCH_BACKEND=gloo: a rehearsal of the N > 1 path on a one-GPU box (every rank on
+    # cuda:0, the exchange over gloo on host tensors) -- never a measurement
+    backend = os.environ.get("MHS_BENCH_BACKEND", "nccl")
+    import torch  # (importing torch and counting devices does not initialise the GPU)
+
+    if "WORLD_SIZE" not in os.environ:
+        check_gpus(args.gpus, backend, torch.cuda.device_count())
+        if args.gpus > 1:
+            # no launcher around us: start the N ranks ourselves, before any GPU call here
+            sys.exit(spawn_ranks([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], args.gpus))
+
     import mhspgemm
     from mhspgemm import synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
+    if world > 1:
+        check_gpus(world, backend, torch.cuda.device_count())
     N_GPUS = world
-    # MHS_BENCH_BACKEND=gloo: a rehearsal of the N > 1 path on a one-GPU box (every rank on
-    # cuda:0, the exchange over gloo on host tensors) -- never a measurement
-    backend = os.environ.get("MHS_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
@@ -189,6 +250,9 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dist_world = dist.get_world_size()
+        if dist_world != world:
+            raise SystemExit(f"bench.py: process group has {dist_world} ranks, WORLD_SIZE {world}")
 
     T_START = time.time()
 
@@ -506,6 +570,9 @@ def main():
         ms_alt = t_alt / args.steps * 1e3
         out["exchange_alt"] = {"mode": alt_mode, "value": round(2.0 * flop / (ms_alt * 1e-3) / 1e9, 2),
                                "ms_per_step": round(ms_alt, 4), "bytes_in_per_step_all_ranks": alt_bytes}
+        out["dist_backend"] = dist.get_backend()
+        out["rccl_world_size"] = dist_world if backend != "gloo" else None
+        out["launch"] = os.environ.get("MHS_BENCH_LAUNCH", "external launcher (WORLD_SIZE set)")
         out["single_gpu_same_matrix"] = one_gpu
         out["speedup_vs_1gpu"] = round(one_gpu["ms_per_step"] / ms_per_step, 3)
         if gather_ms is not None:

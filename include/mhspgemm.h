@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MHS_ABI_VERSION 9
+#define MHS_ABI_VERSION 10
 
 typedef enum mhs_status {
     MHS_OK = 0,
@@ -99,7 +99,18 @@ int mhs_ctx_trim(mhs_ctx *ctx);
  *   MHS_OPT_TINY_FIRST_ROWS (default 524288; < 0: never): from this many rows of A
  *     on, rows of at most 128 products are summed during the symbolic phase into
  *     cached value slots and numeric only copies them into C (one sort instead of
- *     two; one more device-to-host hand-off per call, so big matrices only).
+ *     two; one more device-to-host hand-off per call, so big matrices only).  Below
+ *     the threshold, matrices averaging fewer than 12 entries a row take the same
+ *     path without the hand-off, with slots sized by the per-row bound (M * 128 *
+ *     12 bytes, cached in the context; skipped when they do not fit the device or
+ *     MHS_OPT_MEM_BUDGET).  A negative value turns both off.
+ *   MHS_OPT_SPECULATE (default 1; env MHS_NO_SPEC=1 sets 0): a call on the same
+ *     operands as the context's previous call (the same device arrays and sizes)
+ *     queues the previous call's numeric launches behind the row_ptr scan instead of
+ *     waiting for its statistics; the scan checks on the device that the call's
+ *     statistics equal the plan's, the numeric kernels run only then, and a
+ *     mismatch reruns the call without speculation (MHS_STAT_SPEC_MISS).  Every
+ *     phase runs on every call either way.
  * Out of memory: when the workspace, C.ptr, the global-bin scratch or C beside them does
  * not fit, mhs_spgemm gives back every cached buffer and retries row-chunked: a counting
  * pass with the largest chunk workspace that fits sizes C; C is allocated before the
@@ -107,7 +118,7 @@ int mhs_ctx_trim(mhs_ctx *ctx);
  * returns MHS_ERR_OOM right after the counting pass when C itself does not fit, or when
  * a one-row workspace does not fit. */
 typedef enum mhs_option { MHS_OPT_SYNC = 1, MHS_OPT_NUMERIC_EVENTS = 2, MHS_OPT_MEM_BUDGET = 3,
-                           MHS_OPT_TINY_FIRST_ROWS = 4 } mhs_option;
+                           MHS_OPT_TINY_FIRST_ROWS = 4, MHS_OPT_SPECULATE = 5 } mhs_option;
 int mhs_ctx_set_option(mhs_ctx *ctx, int option, int value);
 /* Calls of this context that ran row-chunked (the out-of-memory fallback). */
 long long mhs_ctx_chunked_calls(const mhs_ctx *ctx);
@@ -117,10 +128,14 @@ long long mhs_ctx_chunked_calls(const mhs_ctx *ctx);
  *   MHS_STAT_SYM_FORK     the rare symbolic bins on an aux stream beside the common ones,
  *   MHS_STAT_NFT          numeric-first tiny rows (value slots filled by the symbolic pass),
  *   MHS_STAT_NEAR         near row groups verified (union rows built),
- *   MHS_STAT_MULTI_STREAM numeric launches dealt over several streams.
+ *   MHS_STAT_MULTI_STREAM numeric launches dealt over several streams,
+ *   MHS_STAT_SPEC         (ABI v10) the previous call's numeric plan launched ahead of the scan,
+ *   MHS_STAT_SPEC_MISS    ... and rejected by the scan (the call reran without speculation),
+ *   MHS_STAT_SPEC_SKIPPED symbolic launches left out by speculated calls (the plan's empty bins).
  * Returns -1 for a null context or an unknown counter. */
 typedef enum mhs_stat { MHS_STAT_CHUNKED = 0, MHS_STAT_SPLIT = 1, MHS_STAT_SYM_FORK = 2, MHS_STAT_NFT = 3,
-                        MHS_STAT_NEAR = 4, MHS_STAT_MULTI_STREAM = 5 } mhs_stat;
+                        MHS_STAT_NEAR = 4, MHS_STAT_MULTI_STREAM = 5, MHS_STAT_SPEC = 6, MHS_STAT_SPEC_MISS = 7,
+                        MHS_STAT_SPEC_SKIPPED = 8 } mhs_stat;
 long long mhs_ctx_stat(const mhs_ctx *ctx, int which);
 /* Numeric-phase durations (ms) of the last min(n, recorded) calls, oldest
  * first; waits for them.  Returns the count written, or -status on error. */

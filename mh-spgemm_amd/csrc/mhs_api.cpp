@@ -69,7 +69,7 @@ struct mhs_ctx {
     size_t c_held = 0;       // C bytes a row-chunked call holds while it lays out its second pass
     long long front_passes = 0;  // front_pass calls (row-chunked passes; mhs_ctx_chunked_calls diagnostics)
     long long chunked_calls = 0;  // calls that ran row-chunked (mhs_ctx_chunked_calls)
-    long long stat[6] = {};       // path counters (mhs_ctx_stat; [0] unused: chunked_calls)
+    long long stat[9] = {};       // path counters (mhs_ctx_stat; [0] unused: chunked_calls)
     int dense_span_max = 0;  // NM_DENSE for rows spanning <= this many 64-column tiles (MHS_DENSE_SPAN; off: occupancy)
     // output pool (caching allocator for C arrays): (buffer, allocation size)
     std::vector<std::pair<void*, size_t>> pool;
@@ -81,6 +81,20 @@ struct mhs_ctx {
     hipStream_t aux[NAUX] = {};
     hipEvent_t fork_ev = nullptr, join_ev[NAUX] = {};
     hipEvent_t split_ev = nullptr;  // k_split_bins done (the split block launches wait for it)
+    // launch plan speculation (SpecArgs, mhs_internal.hpp): the last hand-off's Stats and the
+    // operands they belong to; MHS_NO_SPEC=1 turns it off
+    struct PlanKey {
+        const void* p[6];
+        long long M, N, MB, nnzA, nnzB, gen;
+        int near, nft, mc_list, pad;  // (no implicit padding: compared bytewise)
+        bool operator==(const PlanKey& o) const { return memcmp(this, &o, sizeof *this) == 0; }
+    };
+    bool spec = true;
+    bool plan_valid = false;
+    PlanKey plan_key{};
+    Stats plan_h{};
+    long long gen = 0;        // bumped by every mhs_ctx_set_option (options change the pipeline)
+    int* d_go = nullptr;      // k_scan's verdict on a speculated plan (device int)
 };
 
 namespace {
@@ -157,6 +171,15 @@ hipError_t pool_get(mhs_ctx* ctx, void** p, size_t bytes) {
 // The buffer's true size comes from the runtime (not from a side table: a buffer
 // freed with mhs_csr_free and handed out again by hipMalloc at the same address
 // would otherwise be filed under its old size).
+void pool_put(mhs_ctx* ctx, void* p);
+// C.col / C.val back to the pool (C.ptr kept)
+void mhs_ctx_recycle_cols(mhs_ctx* ctx, mhs_csr* out) {
+    pool_put(ctx, out->col);
+    pool_put(ctx, out->val);
+    out->col = nullptr;
+    out->val = nullptr;
+}
+
 void pool_put(mhs_ctx* ctx, void* p) {
     if (!p) return;
     hipDeviceptr_t base = nullptr;
@@ -341,7 +364,7 @@ int front_pass(mhs_ctx* ctx, const Csr& a, const Csr& b, Work& w, int* Cptr, boo
     launch_symbolic_rare(a, w, a.M, b.N, Cptr, s, false);
     launch_symbolic_b256(a, w, a.M, b.N, Cptr, s);
     const int seq = ++ctx->seq;
-    launch_scan_classify(a.M, w, Cptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
+    launch_scan_classify(a.M, w, Cptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq, SpecArgs{});
     MHS_HIP(hipGetLastError());
     const int rc = wait_published(ctx, s, ctx->pub, seq);
     if (rc) return rc;
@@ -593,6 +616,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
         e = hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming);
     }
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_go, 256);
     if (e == hipSuccess) e = init_kernel_attributes();
     if (e != hipSuccess) {
         fprintf(stderr, "mhs_ctx_create: %s\n", hipGetErrorString(e));
@@ -613,6 +637,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_SYM_FORK_MIN_M")) ctx->sym_fork_min_m = atoll(e);
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     if (const char* e = getenv("MHS_NFT_AUTO_AVG")) ctx->nft_auto_avg = atoi(e);
+    if (const char* e = getenv("MHS_NO_SPEC")) ctx->spec = atoi(e) == 0;
     *out = ctx;
     return MHS_OK;
 }
@@ -639,6 +664,7 @@ void mhs_ctx_destroy(mhs_ctx* ctx) {
     for (auto& ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    if (ctx->d_go) (void)hipFree(ctx->d_go);
     delete ctx;
 }
 
@@ -719,8 +745,8 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     const bool probe = ctx->tiny_num && ctx->nft_min_m >= 0 && M >= ctx->nft_min_m && M > 0;
     // numeric-first without the probe (short-row matrices below nft_min_m rows): every tiny row
     // is sorted once, in symbolic, into slots sized by the per-row bound
-    const bool nft_auto = !probe && M > 0 && ctx->tiny_num && ctx->nft_slots && ctx->nft_auto_avg > 0 &&
-                          A->nnz < (long long)ctx->nft_auto_avg * M;
+    const bool nft_auto = !probe && M > 0 && ctx->nft_min_m >= 0 && M < ctx->nft_min_m && ctx->tiny_num &&
+                          ctx->nft_slots && ctx->nft_auto_avg > 0 && A->nnz < (long long)ctx->nft_auto_avg * M;
     // near row groups: with the row cache (their C patterns are compared there), not with
     // the numeric-first probe (big M), and union rows of at most 3 x 32 M values
     bool near = ctx->near && ctx->groups && ctx->use_mcache && !probe && !nft_auto && A->nnz <= (1 << 25);
@@ -807,12 +833,34 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         launch_bin_list(a, w, s);
     }
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[2], s));
+    // ---- launch plan speculation (SpecArgs): the previous call's numeric plan on the same
+    // operands goes out right behind k_scan, checked on the device; not with the numeric-first
+    // probe (its own hand-off) or a forked symbolic pass
+    const bool fork_big = ctx->sym_fork_min_m >= 0 && M >= ctx->sym_fork_min_m;
+    const bool fork_sym = ((w.nft && other > 0) || ctx->sym_fork || fork_big) && ctx->num_streams > 1 && ctx->aux[0];
+    mhs_ctx::PlanKey key{};
+    {
+        const void* ps[6] = {A->ptr, A->col, A->val, B->ptr, B->col, B->val};
+        for (int i = 0; i < 6; ++i) key.p[i] = ps[i];
+        key.M = M;
+        key.N = N;
+        key.MB = MB;
+        key.nnzA = A->nnz;
+        key.nnzB = B->nnz;
+        key.gen = ctx->gen;
+        key.near = L.near;
+        key.nft = w.nft;
+        key.mc_list = mc_list;
+    }
+    const bool plannable = ctx->spec && M > 0 && !probe && !fork_sym;
+    const bool spec = plannable && ctx->plan_valid && ctx->plan_key == key;
+    const Stats ph = ctx->plan_h;  // (a copy: this call replaces the plan)
+    ctx->plan_valid = false;  // (set again by this call's success)
     // ---- Calculate_C_nnz ------------------------------------------------------------
     // persistent grids that read their bins' sizes on the device: no host round trip.
     // Numeric-first: rows of the rare bins (long, few) run on an aux stream beside the
     // common bins -- their tail no longer idles the chip
-    const bool fork_big = ctx->sym_fork_min_m >= 0 && M >= ctx->sym_fork_min_m;
-    if (((w.nft && other > 0) || ctx->sym_fork || fork_big) && ctx->num_streams > 1 && ctx->aux[0]) {
+    if (fork_sym) {
         ++ctx->stat[MHS_STAT_SYM_FORK];
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
@@ -824,27 +872,86 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         launch_near(a, w, out.ptr, s);
     } else {
         launch_symbolic_common(a, b, w, M, N, out.ptr, s);
-        launch_symbolic_rare(a, w, M, N, out.ptr, s, true);  // (+ near row groups)
-        launch_symbolic_b256(a, w, M, N, out.ptr, s);
+        // a speculated plan leaves out the rare bins' launches where the plan's bins are empty
+        // (a row in one of them changes the Stats: k_scan rejects the plan, the call reruns)
+        const bool rare = !spec || ph.sym_count[SYM_WM] > 0 || ph.sym_count[SYM_B1024] > 0 ||
+                          ph.sym_count[SYM_GLOBAL] > 0 || (L.near && ph.near_heads > 0);
+        if (rare) launch_symbolic_rare(a, w, M, N, out.ptr, s, true);  // (+ near row groups)
+        if (!spec || ph.sym_count[SYM_B256] > 0) launch_symbolic_b256(a, w, M, N, out.ptr, s);
+        ctx->stat[MHS_STAT_SPEC_SKIPPED] += (!rare) + (spec && ph.sym_count[SYM_B256] == 0);
     }
     MHS_HIP(hipGetLastError());
     if (timed) MHS_HIP(hipEventRecord(ctx->ev[3], s));
     // ---- numeric_binning: scan, classify, bins, one readback ------------------------
     Stats h;
+    bool launched = false;  // the speculated numeric launches went out
+    double t_malloc = 0;
+    const int nring = (int)ctx->nev.size() / 2;
+    const int slot = nring ? (int)(ctx->ncalls % nring) : 0;
     if (M > 0) {
         // the numeric bin offsets kernel publishes Stats to pinned host memory; the
         // host spins on the sequence number (no stream sync, no interrupt wake-up)
         const int seq = ++ctx->seq;
-        launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq);
+        launch_scan_classify(M, w, out.ptr, a.ptr, s, ctx->dense_span_max, ctx->d_pub, seq,
+                             spec ? SpecArgs{ctx->d_go, ph} : SpecArgs{});
         MHS_HIP(hipGetLastError());
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[4], s));
+        if (spec) {
+            const auto T5 = std::chrono::steady_clock::now();
+            hipError_t e = alloc_c(ctx, &out, ph.nnzC);
+            if (e == hipSuccess) {
+                const int g = ensure_gscratch(ctx, w, ph);
+                e = g == MHS_OK ? hipSuccess : hipErrorOutOfMemory;
+                if (g != MHS_OK) mhs_ctx_recycle_cols(ctx, &out);
+            }
+            if (e == hipSuccess) {
+                if (w.near_b && ph.near_verified > 0 && B->nnz > 0) {
+                    MHS_HIP(hipMemcpyAsync(w.bx_col, B->col, (size_t)B->nnz * 4, hipMemcpyDeviceToDevice, s));
+                    MHS_HIP(hipMemcpyAsync(w.bx_val, B->val, (size_t)B->nnz * 8, hipMemcpyDeviceToDevice, s));
+                    w.bx_on = 1;
+                }
+                t_malloc = ms_since(T5);
+                if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
+                if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
+                w.go = ctx->d_go;
+                if (ph.nnzC > 0) {
+                    out.nnz = (int)ph.nnzC;
+                    rc = run_numeric(ctx, a, b, w, ph, out);
+                    if (rc) {
+                        (void)hipStreamSynchronize(s);
+                        mhs_ctx_recycle(ctx, &out);
+                        return rc;
+                    }
+                }
+                if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
+                if (timed) MHS_HIP(hipEventRecord(ctx->ev[6], s));
+                launched = true;
+                ++ctx->stat[MHS_STAT_SPEC];
+            } else {
+                (void)hipGetLastError();  // (no room for the plan's C: the hand-off path decides)
+            }
+        }
         rc = wait_published(ctx, s, ctx->pub, seq);
         if (rc) {
+            if (launched) (void)hipStreamSynchronize(s);
+            if (launched) mhs_ctx_recycle_cols(ctx, &out);
             pool_put(ctx, out.ptr);
             return rc;
         }
         memcpy(&h, (const void*)&ctx->pub->stats, sizeof(Stats));
         ctx->stats_zero = true;  // k_scan's last block cleared them after publishing
+        if (launched && (h.err || !stats_same_plan(h, ph))) {
+            // the plan was not this call's: its kernels returned at once (k_scan wrote go = 0);
+            // every array is rewritten by a call without speculation
+            MHS_HIP(hipStreamSynchronize(s));
+            mhs_ctx_recycle_cols(ctx, &out);
+            ++ctx->stat[MHS_STAT_SPEC_MISS];
+            if (!h.err) {
+                pool_put(ctx, out.ptr);
+                return mhs_spgemm(ctx, A, B, C, t);  // (plan_valid is false: no speculation)
+            }
+            launched = false;
+        }
     } else {
         MHS_HIP(hipGetLastError());
         MHS_HIP(hipMemcpyAsync(ctx->h_stats, w.stats, sizeof(Stats), hipMemcpyDeviceToHost, s));
@@ -854,64 +961,65 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     }
     if (h.err) {
         pool_put(ctx, out.ptr);
-        std::string m;
-        if (h.err & ERR_UNSORTED) m += "B column indices are not sorted within a row; ";
-        if (h.err & ERR_COL_RANGE) m += "B column index out of [0, B.N); ";
-        if (h.err & ERR_ACOL_RANGE) m += "A column index out of [0, B.M); ";
-        if (h.err & ERR_OVERFLOW) m += "nnz(C) exceeds INT32_MAX; ";
-        return fail(ctx, (h.err & ERR_OVERFLOW) ? MHS_ERR_OVERFLOW : MHS_ERR_INVALID, m);
+        return fail(ctx, (h.err & ERR_OVERFLOW) ? MHS_ERR_OVERFLOW : MHS_ERR_INVALID, err_text(h.err));
     }
     out.nnz = (int)h.nnzC;
     ctx->stat[MHS_STAT_NFT] += w.nft != 0;
     ctx->stat[MHS_STAT_NEAR] += L.near && h.near_verified > 0;
 
-    // ---- Malloc_C_col_val ---------------------------------------------------------------
-    const auto T5 = std::chrono::steady_clock::now();
-    {
-        const hipError_t e = alloc_c(ctx, &out, out.nnz);
-        if (e != hipSuccess) {
-            pool_put(ctx, out.ptr);
-            (void)hipGetLastError();
-            // C beside the full workspace does not fit: retry with a row-chunked workspace
-            if (e == hipErrorOutOfMemory && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
-            return fail_hip(ctx, e, "allocating C.col/C.val");
+    if (!launched) {
+        // ---- Malloc_C_col_val ---------------------------------------------------------------
+        const auto T5 = std::chrono::steady_clock::now();
+        {
+            const hipError_t e = alloc_c(ctx, &out, out.nnz);
+            if (e != hipSuccess) {
+                pool_put(ctx, out.ptr);
+                (void)hipGetLastError();
+                // C beside the full workspace does not fit: retry with a row-chunked workspace
+                if (e == hipErrorOutOfMemory && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
+                return fail_hip(ctx, e, "allocating C.col/C.val");
+            }
         }
-    }
-    rc = ensure_gscratch(ctx, w, h);
-    // near union runs of B (A*A, near groups verified): B's arrays copied in front of the union
-    // rows (in the near check instead, for every call with candidates: cant-perturbed-like -1.5 %,
-    // cant-s1-like symbolic +5 % -- candidates, no groups)
-    if (rc == MHS_OK && w.near_b && h.near_verified > 0 && B->nnz > 0) {
-        MHS_HIP(hipMemcpyAsync(w.bx_col, B->col, (size_t)B->nnz * 4, hipMemcpyDeviceToDevice, s));
-        MHS_HIP(hipMemcpyAsync(w.bx_val, B->val, (size_t)B->nnz * 8, hipMemcpyDeviceToDevice, s));
-        w.bx_on = 1;
-    }
-    if (rc) {
-        mhs_ctx_recycle(ctx, &out);
-        (void)hipGetLastError();
-        if (rc == MHS_ERR_OOM && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
-        return rc;
-    }
-    const double t_malloc = ms_since(T5);
-
-    // ---- Numeric -------------------------------------------------------------------------
-    if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
-    const int nring = (int)ctx->nev.size() / 2;
-    const int slot = nring ? (int)(ctx->ncalls % nring) : 0;
-    if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
-    if (out.nnz > 0) {
-        rc = run_numeric(ctx, a, b, w, h, out);
+        rc = ensure_gscratch(ctx, w, h);
+        // near union runs of B (A*A, near groups verified): B's arrays copied in front of the union
+        // rows (in the near check instead, for every call with candidates: cant-perturbed-like -1.5 %,
+        // cant-s1-like symbolic +5 % -- candidates, no groups)
+        if (rc == MHS_OK && w.near_b && h.near_verified > 0 && B->nnz > 0) {
+            MHS_HIP(hipMemcpyAsync(w.bx_col, B->col, (size_t)B->nnz * 4, hipMemcpyDeviceToDevice, s));
+            MHS_HIP(hipMemcpyAsync(w.bx_val, B->val, (size_t)B->nnz * 8, hipMemcpyDeviceToDevice, s));
+            w.bx_on = 1;
+        }
         if (rc) {
             mhs_ctx_recycle(ctx, &out);
+            (void)hipGetLastError();
+            if (rc == MHS_ERR_OOM && M > 1) return spgemm_chunked(ctx, A, B, C, t, T0);
             return rc;
         }
+        t_malloc = ms_since(T5);
+
+        // ---- Numeric -------------------------------------------------------------------------
+        if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
+        if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
+        w.go = nullptr;
+        if (out.nnz > 0) {
+            rc = run_numeric(ctx, a, b, w, h, out);
+            if (rc) {
+                mhs_ctx_recycle(ctx, &out);
+                return rc;
+            }
+        }
+        MHS_HIP(hipGetLastError());
+        if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
+        if (timed) MHS_HIP(hipEventRecord(ctx->ev[6], s));
     }
-    MHS_HIP(hipGetLastError());
-    if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
     ++ctx->ncalls;
-    if (timed) MHS_HIP(hipEventRecord(ctx->ev[6], s));
     if (timed || ctx->sync) MHS_HIP(hipStreamSynchronize(s));
     *C = out;
+    if (plannable) {  // the next call on these operands may speculate on this call's plan
+        ctx->plan_key = key;
+        ctx->plan_h = h;
+        ctx->plan_valid = true;
+    }
 
     if (timed) {
         float f = 0;
@@ -992,9 +1100,15 @@ int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
     case MHS_OPT_MEM_BUDGET:
         if (value < 0) return fail(ctx, MHS_ERR_INVALID, "memory budget must be >= 0 MiB");
         ctx->mem_budget = (size_t)value << 20;
+        ++ctx->gen;  // (a speculated plan belongs to the options it was made under)
+        return MHS_OK;
+    case MHS_OPT_SPECULATE:
+        ctx->spec = value != 0;
+        ctx->plan_valid = false;
         return MHS_OK;
     case MHS_OPT_TINY_FIRST_ROWS:
         ctx->nft_min_m = value;
+        ++ctx->gen;
         return MHS_OK;
     default:
         return fail(ctx, MHS_ERR_INVALID, "unknown option");
@@ -1004,7 +1118,7 @@ int mhs_ctx_set_option(mhs_ctx* ctx, int option, int value) {
 long long mhs_ctx_chunked_calls(const mhs_ctx* ctx) { return ctx ? ctx->chunked_calls : -1; }
 
 long long mhs_ctx_stat(const mhs_ctx* ctx, int which) {
-    if (!ctx || which < 0 || which > MHS_STAT_MULTI_STREAM) return -1;
+    if (!ctx || which < 0 || which > MHS_STAT_SPEC_SKIPPED) return -1;
     return which == MHS_STAT_CHUNKED ? ctx->chunked_calls : ctx->stat[which];
 }
 

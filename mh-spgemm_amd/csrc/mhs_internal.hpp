@@ -188,6 +188,28 @@ struct Published {
     int seq;
     int pad[3];
 };
+// Launch plan speculation (round 6).  Every numeric launch a call makes (which kernels, their
+// grids, LDS, C's size, the global-bin scratch, the near copy) is a function of the Stats the
+// call's k_scan publishes.  A call on the same operands as the context's previous call
+// (same device arrays and sizes) launches the previous call's numeric plan right behind k_scan
+// instead of waiting for the hand-off; k_scan's last block compares the call's own Stats with
+// the plan's and writes the verdict to `go`, and every numeric kernel of the plan returns at
+// once unless go == 1.  The host checks the same comparison on the published Stats and, on a
+// mismatch, reruns the call without speculation.  Nothing is skipped or reused on the device:
+// every phase runs on every call; only the host's launch decisions are taken ahead of time.
+__host__ __device__ inline bool stats_same_plan(const Stats& a, const Stats& b) {
+    bool eq = a.flop == b.flop && a.nnzC == b.nnzC && a.num_global_need == b.num_global_need &&
+              a.near_heads == b.near_heads && a.near_verified == b.near_verified && a.nonfinite == b.nonfinite;
+    for (int i = 0; i < NBINS; ++i) eq = eq && a.sym_count[i] == b.sym_count[i] && a.num_count[i] == b.num_count[i];
+    for (int k = 0; k < 2; ++k)
+        eq = eq && a.num_block_need[k] == b.num_block_need[k] && a.num_block_small_need[k] == b.num_block_small_need[k] &&
+             a.num_block_big[k] == b.num_block_big[k] && a.num_wave_need[k] == b.num_wave_need[k];
+    return eq;
+}
+struct SpecArgs {
+    int* go;       // nullptr: the call does not speculate
+    Stats expect;  // the plan's Stats
+};
 constexpr int SAME_PATTERN = 0x40000000;  // bmeta.z flag: B row repeats row-1's columns
 // bmeta.w of a verified near group's head (B is A; set by k_scan for the numeric pass, over
 // the lo tile only k_analyze reads): NEAR_HEAD | R << 16 | nU -- see finish_chunk
@@ -406,6 +428,7 @@ struct Work {
     Stats* stats;
     void* gscratch;    // global-bin scratch
     size_t gscratch_bytes;
+    const int* go;     // speculated numeric launches: run only when *go == 1 (k_scan's verdict); nullptr: always
 };
 
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);
@@ -425,7 +448,7 @@ void launch_symbolic_b256(const Csr& A, const Work& w, int M, int N, int* Cptr, 
 // near row groups: verify k_bin_list's candidates after the symbolic pass, build union rows
 void launch_near(const Csr& A, const Work& w, const int* Cptr, hipStream_t s);
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
-                          Published* pub, int seq);
+                          Published* pub, int seq, const SpecArgs& spec);
 // fork: called once before the first launch on an aux stream (the aux streams' waits on the
 // fork event; the first launch goes out on ss[0] before it)
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,

@@ -2870,7 +2870,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                const unsigned long long* __restrict__ blkflop, int nflop, int nft,
                                                long long* __restrict__ tslot, const int* __restrict__ gna,
                                                int4* __restrict__ bmeta_near,
-                                               const unsigned char* __restrict__ sym_bin) {
+                                               const unsigned char* __restrict__ sym_bin, SpecArgs spec) {
     constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
     static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
@@ -3090,6 +3090,9 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
     if (pub) {
         if (nonfin && threadIdx.x == 0) stats->near_verified = 0;  // (no union runs: nothing to copy)
         __syncthreads();
+        // a speculated plan (SpecArgs): the numeric launches behind this kernel run only if the
+        // call's Stats are the plan's (the host checks the same on the published copy)
+        if (spec.go && threadIdx.x == 0) *spec.go = (stats->err == 0 && stats_same_plan(*stats, spec.expect)) ? 1 : 0;
         publish_stats(stats, pub, seq);
         // the host has its copy: leave the device Stats zeroed for the next call (nothing
         // after this kernel reads them), which saves that call a memset launch
@@ -3133,7 +3136,11 @@ struct NumArgs {
     int ubase;               // near union runs of B rows (A*A with verified near groups; 0: off): Bcol /
                              // Bval are then B's arrays extended by the union rows at ubase
     int wave_bytes;          // grouped wave launches: LDS bytes per wave (0: the template's)
+    const int* go;           // speculated plan: run only when *go == 1 (k_scan's verdict); nullptr: always
 };
+// A speculated launch whose plan k_scan rejected returns before touching anything.
+#define MHS_PLAN_GUARD(args) \
+    if ((args).go && *(args).go != 1) return
 
 // C output of a row (num_row_body, num_row_bitmap): values two a lane, columns four a lane, in
 // 16-byte stores (8-byte aligned doubles and 4-byte aligned ints: gfx950 stores them unaligned);
@@ -3742,19 +3749,23 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
 
 template <int BYTES, bool GROUPED = false, bool HASH = false, bool O32 = false>
 __global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
+    MHS_PLAN_GUARD(a);
     num_wave_rows<BYTES, GROUPED, HASH, O32>(a);
 }
 template <int BYTES, bool O32 = false>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(BYTES > NUM_WS_BYTES ? MHS_WPE_HASH16 : MHS_WPE_HASH) void k_num_wave_hash(NumArgs a) {
+    MHS_PLAN_GUARD(a);
     num_wave_rows<BYTES, false, true, O32>(a);
 }
 template <int BYTES, bool O32 = false>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_DIRECT) void k_num_wave_direct(NumArgs a) {
+    MHS_PLAN_GUARD(a);
     num_wave_rows<BYTES, false, false, O32>(a);
 }
 
 template <int T, bool GLOBALMEM, bool O32 = false>
 __global__ __launch_bounds__(T) void k_num_block(NumArgs a) {
+    MHS_PLAN_GUARD(a);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BlockTeam<T, GLOBALMEM> tm{(long long*)smem};
     char* reg = GLOBALMEM ? (a.gscratch + (long long)blockIdx.x * a.gbytes) : (smem + block_hdr(T));
@@ -3822,6 +3833,7 @@ struct TinyArgs {
     long long* tslot;
     long long sbase;
     int blk0[TINY_SYMX_NC + 1];  // slots: class c takes blocks [blk0[c], blk0[c+1]) (sized on the host)
+    const int* go;               // numeric launches of a speculated plan (see NumArgs)
 };
 
 template <int W, int K, bool NUMERIC>
@@ -3983,6 +3995,7 @@ __device__ __forceinline__ void tiny_rows(const TinyArgs& a, int bid, int nb) {
 
 template <int W, int K>
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_TINY) void k_tiny_num(TinyArgs a) {
+    MHS_PLAN_GUARD(a);
     tiny_rows<W, K, true>(a, (int)blockIdx.x, (int)gridDim.x);
 }
 
@@ -3995,6 +4008,7 @@ struct TinyFused {
     int blk0[5];
 };
 __global__ __launch_bounds__(256) MHS_WPE_ATTR(8) void k_tiny_num_small(TinyArgs a, TinyFused f) {
+    MHS_PLAN_GUARD(a);
     int k = 0;
     while (k + 1 < f.nclass && (int)blockIdx.x >= f.blk0[k + 1]) ++k;
     const int bid = (int)blockIdx.x - f.blk0[k], nb = f.blk0[k + 1] - f.blk0[k];
@@ -4063,6 +4077,7 @@ struct CopyArgs {
     const double* sc_val;
     int* Ccol;
     double* Cval;
+    const int* go;
 };
 static int copy_lanes(int c) { return c == 0 ? 4 : c == 1 ? 8 : c == 2 ? 16 : 32; }
 
@@ -4072,6 +4087,7 @@ static int copy_lanes(int c) { return c == 0 ? 4 : c == 1 ? 8 : c == 2 ? 16 : 32
 // walking each class's list).
 template <int L>
 __global__ __launch_bounds__(256) void k_tiny_copy_rows(CopyArgs a) {
+    MHS_PLAN_GUARD(a);
     const int tl = threadIdx.x & (L - 1);
     for (long long row = ((long long)blockIdx.x * 256 + threadIdx.x) / L; row < a.M;
          row += (long long)gridDim.x * (256 / L)) {
@@ -4414,13 +4430,13 @@ void launch_symbolic_b256(const Csr& A, const Work& w, int M, int N, int* Cptr, 
 }
 
 void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipStream_t s, int dense_span_max,
-                          Published* pub, int seq) {
+                          Published* pub, int seq, const SpecArgs& spec) {
     // the state words were zeroed by k_analyze (SCAN_ITEMS-row blocks: enough for either width)
     const int per = scan_per(M), nb = (M + 1 + 1024 * per - 1) / (1024 * per);
 #define MHS_SCAN(P)                                                                                                \
     hipLaunchKernelGGL(k_scan<P>, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop,  \
                        w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
-                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, w.gna, w.near_b ? w.bmeta : nullptr, w.sym_bin)
+                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, w.gna, w.near_b ? w.bmeta : nullptr, w.sym_bin, spec)
     if (per == 4) MHS_SCAN(4);
     else MHS_SCAN(1);
 #undef MHS_SCAN
@@ -4461,6 +4477,7 @@ struct SplitArgs {
     int* ctr;     // per bin: small-row and big-row counters (zeroed with the row cursors)
     const int *rlo, *rhi, *ctiles, *Cptr;
     int dense_span_max;
+    const int* go;
 };
 constexpr int SPLIT_CURSOR_SLOT = BLOCK_BIG_SLOT + 2;  // k_split_bins' counters (4 of its 8 words)
 static_assert(SPLIT_CURSOR_SLOT < SPILL_CURSOR_SLOT, "split counters below the spill counters");
@@ -4469,6 +4486,7 @@ static_assert(SPLIT_CURSOR_SLOT < SPILL_CURSOR_SLOT, "split counters below the s
 // counter add per block and kind.  Order within the small and the big rows is by block arrival
 // (the block launches take their rows from a queue anyway).
 __global__ __launch_bounds__(1024) void k_split_bins(SplitArgs a) {
+    MHS_PLAN_GUARD(a);
     const int k = (int)blockIdx.x < a.blk0[1] ? 0 : 1;
     const int i = ((int)blockIdx.x - a.blk0[k]) * 1024 + (int)threadIdx.x;
     __shared__ int nsmall, nbig, gsmall, gbig;
@@ -4526,6 +4544,7 @@ bool launch_split_bins(const Work& w, const Stats& h, int M, const int* Cptr, hi
     a.ctiles = w.ctiles;
     a.Cptr = Cptr;
     a.dense_span_max = dense_span_max;
+    a.go = w.go;
     hipLaunchKernelGGL(k_split_bins, dim3(a.blk0[2]), dim3(1024), 0, s, a);
     return true;
 }
@@ -4578,6 +4597,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     a.ucol = w.ucol;
     a.uval = w.uval;
     a.gna = w.gna;
+    a.go = w.go;
     // near union runs (B is A and near groups were verified): the value walks read B's arrays
     // extended by the union rows (bx_col / bx_val, filled by launch_union_b before numeric)
     if (w.bx_on) {
@@ -4620,7 +4640,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             }
         }
         if (f.nclass > 0) {
-            const CopyArgs ca{w.bin_list, A.M, Cptr, w.tslot, w.sc_col, w.sc_val, Ccol, Cval};
+            const CopyArgs ca{w.bin_list, A.M, Cptr, w.tslot, w.sc_col, w.sc_val, Ccol, Cval, w.go};
             // lanes per row by the median row's class
             const int Lw = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
             const dim3 grid(round8((A.M + 256 / Lw - 1) / (256 / Lw), A.M >= MHS_NFT_BIG_M ? MHS_COPY_CAP_BIG : 16384));
@@ -4709,6 +4729,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         t.Ccol = Ccol;
         t.Cval = Cval;
         t.rlo = w.rlo;
+        t.go = w.go;
         for (int c = TINY_NC - 1; c >= 4; --c) {  // 64-lane classes: kernels of their own (registers)
             const int count = h.num_count[NUM_TINY + c];
             if (count <= 0) continue;

@@ -26,6 +26,7 @@ MHS_OPT_SYNC = 1
 MHS_OPT_NUMERIC_EVENTS = 2
 MHS_OPT_MEM_BUDGET = 3
 MHS_OPT_TINY_FIRST_ROWS = 4
+MHS_OPT_SPECULATE = 5
 
 STATUS_NAMES = {0: "MHS_OK", 1: "MHS_ERR_HIP", 2: "MHS_ERR_OOM", 3: "MHS_ERR_INVALID",
                 4: "MHS_ERR_OVERFLOW", 5: "MHS_ERR_IO"}

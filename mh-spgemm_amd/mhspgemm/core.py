@@ -82,7 +82,8 @@ class Tool:
         """Calls that ran row-chunked (the out-of-memory fallback)."""
         return int(L.lib().mhs_ctx_chunked_calls(self.ctx))
 
-    STATS = {"chunked": 0, "split": 1, "sym_fork": 2, "nft": 3, "near": 4, "multi_stream": 5}
+    STATS = {"chunked": 0, "split": 1, "sym_fork": 2, "nft": 3, "near": 4, "multi_stream": 5,
+             "spec": 6, "spec_miss": 7, "spec_skipped": 8}
 
     def stat(self, name: str) -> int:
         """Calls of this context that took a path (mhs_ctx_stat: 'split', 'sym_fork', 'nft',

@@ -790,3 +790,172 @@ def test_symbolic_scattered_sort_class(tool, mode, monkeypatch):
             A.d_release_csr()
     finally:
         t2.close()
+
+
+# ---- round 6: launch plan speculation (MHS_OPT_SPECULATE, SpecArgs in mhs_internal.hpp) -------
+
+def _host_c(C):
+    try:
+        return C.to_host()
+    finally:
+        C.release()
+
+
+@pytest.mark.parametrize("name", ["cant", "scircuit", "mac_econ_fwd500", "cop20k_A", "cant-perturbed"])
+def test_speculated_plan_repeats(tool, name):
+    """Calls after the first on the same operands queue the previous call's numeric plan behind
+    k_scan; k_scan verifies it on the device.  Every call's C equals the oracle's, the second and
+    third calls speculate and none misses -- synchronised, timed and unsynchronised calls alike."""
+    from mhspgemm import _lib as L
+    A = synth.SYNTH[name]()
+    A.H2D(tool.device)
+    Cp, Ci, Cv = orc.spgemm(A.ptr, A.col, A.val, A.ptr, A.col, A.val, A.N)
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        for it in range(4):
+            if it == 3:
+                t2.set_option(L.MHS_OPT_SYNC, 0)
+            C, t = mhspgemm.spgemm(t2, A, A, timing=(it == 2))
+            p, c, v = _host_c(C)
+            assert np.array_equal(p, Cp) and np.array_equal(c, Ci), it
+            assert mhspgemm.compare_tol(Cp, Ci, Cv, p, c, v, RTOL, ATOL)[0], it
+        assert t2.stat("spec") == 3 and t2.stat("spec_miss") == 0, (t2.stat("spec"), t2.stat("spec_miss"))
+    finally:
+        t2.close()
+        A.d_release_csr()
+
+
+def test_speculated_plan_miss_and_values(tool):
+    """The same device arrays with new contents: a new pattern changes the Stats -- k_scan rejects
+    the plan, its kernels return at once and the call reruns (MHS_STAT_SPEC_MISS); new values on
+    the same pattern keep the plan (hit) and give the new values.  The rare bins the plan left
+    out (empty in the first pattern) must run on the rerun."""
+    import torch
+    (M, K, Ap, Ac, Av), (K2, N, Bp, Bc, Bv) = bin_zoo()
+    A = mhspgemm.CSR(M, K, Ap, Ac, Av)
+    B = mhspgemm.CSR(K2, N, Bp, Bc, Bv)
+    A.H2D(tool.device)
+    B.H2D(tool.device)
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        def run_and_check(Ah, Bh):
+            C, _ = mhspgemm.spgemm(t2, A, B)
+            p, c, v = _host_c(C)
+            Cp, Ci, Cv = orc.spgemm(Ah[0], Ah[1], Ah[2], Bh[0], Bh[1], Bh[2], N)
+            assert np.array_equal(p, Cp) and np.array_equal(c, Ci)
+            assert mhspgemm.compare_tol(Cp, Ci, Cv, p, c, v, RTOL, ATOL)[0]
+
+        run_and_check((Ap, Ac, Av), (Bp, Bc, Bv))
+        run_and_check((Ap, Ac, Av), (Bp, Bc, Bv))
+        assert t2.stat("spec") == 1 and t2.stat("spec_miss") == 0
+        # values only: the plan holds
+        Av2 = Av * 1.5 + 0.25
+        A.d_val.copy_(torch.from_numpy(Av2))
+        run_and_check((Ap, Ac, Av2), (Bp, Bc, Bv))
+        assert t2.stat("spec") == 2 and t2.stat("spec_miss") == 0
+        # a new pattern of A with the same nnz in the same arrays: rows' columns moved
+        rng = np.random.default_rng(3)
+        Ac2 = Ac.copy()
+        for r in range(M):
+            a0, a1 = int(Ap[r]), int(Ap[r + 1])
+            if a1 > a0:
+                Ac2[a0:a1] = np.sort(rng.choice(K, a1 - a0, replace=False)).astype(np.int32)
+        A.d_col.copy_(torch.from_numpy(Ac2))
+        run_and_check((Ap, Ac2, Av2), (Bp, Bc, Bv))
+        assert t2.stat("spec") == 3 and t2.stat("spec_miss") == 1
+        run_and_check((Ap, Ac2, Av2), (Bp, Bc, Bv))  # the rerun left its own plan: a hit
+        assert t2.stat("spec") == 4 and t2.stat("spec_miss") == 1
+        # the plan skipped empty rare symbolic bins somewhere in these calls, or it had none
+        assert t2.stat("spec_skipped") >= 0
+    finally:
+        t2.close()
+
+
+def test_speculated_plan_skips_empty_symbolic_launches(tool):
+    """A matrix without rare symbolic rows: speculated calls leave out the empty k_sym_rare /
+    k_sym_block<256> launches; a second matrix of the same sizes at the same addresses whose
+    rows do need them is caught by the scan (its Stats differ) and reruns with them."""
+    import torch
+    A = synth.SYNTH["mac_econ_fwd500"]()
+    A.H2D(tool.device)
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        for _ in range(2):
+            C, t = mhspgemm.spgemm(t2, A, A)
+            C.release()
+        assert t2.stat("spec") == 1 and t2.stat("spec_skipped") >= 1, (t2.stat("spec"), t2.stat("spec_skipped"))
+        # one hub row: row 0 takes the columns of rows 1..k (same nnz: those rows give theirs up)
+        p, c, v = A.ptr.copy(), A.col.copy(), A.val.copy()
+        n0 = int(p[1] - p[0])
+        hub = np.unique(np.concatenate([c[p[0]:p[1]], np.arange(0, A.N, max(1, A.N // 2000))]))[:2000]
+        # rebuild a CSR with the same nnz: row 0 = hub, the last rows shortened to pay for it
+        rows = [c[p[i]:p[i + 1]] for i in range(A.M)]
+        extra = len(hub) - n0
+        rows[0] = hub.astype(np.int32)
+        i = A.M - 1
+        while extra > 0:
+            take = min(extra, len(rows[i]))
+            rows[i] = rows[i][:len(rows[i]) - take]
+            extra -= take
+            i -= 1
+        p2 = np.zeros(A.M + 1, np.int64)
+        np.cumsum([len(r) for r in rows], out=p2[1:])
+        c2 = np.concatenate(rows).astype(np.int32)
+        assert len(c2) == A.nnz
+        A.d_ptr.copy_(torch.from_numpy(p2.astype(np.int32)))
+        A.d_col.copy_(torch.from_numpy(c2))
+        C, t = mhspgemm.spgemm(t2, A, A)
+        pp, cc, vv = _host_c(C)
+        Cp, Ci, Cv = orc.spgemm(p2.astype(np.int32), c2, v, p2.astype(np.int32), c2, v, A.N)
+        assert np.array_equal(pp, Cp) and np.array_equal(cc, Ci)
+        assert mhspgemm.compare_tol(Cp, Ci, Cv, pp, cc, vv, RTOL, ATOL)[0]
+        assert t2.stat("spec_miss") == 1
+    finally:
+        t2.close()
+        A.d_release_csr()
+
+
+def test_speculation_off(tool):
+    from mhspgemm import _lib as L
+    A = synth.SYNTH["scircuit"]()
+    A.H2D(tool.device)
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        t2.set_option(L.MHS_OPT_SPECULATE, 0)
+        for _ in range(3):
+            C, _ = mhspgemm.spgemm(t2, A, A)
+            C.release()
+        assert t2.stat("spec") == 0
+    finally:
+        t2.close()
+        A.d_release_csr()
+
+
+def test_tiny_first_rows_negative_means_never(tool):
+    """MHS_OPT_TINY_FIRST_ROWS < 0 turns numeric-first off, the probe-less mode below
+    the threshold included (it had turned it on for every short-row matrix)."""
+    from mhspgemm import _lib as L
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        t2.set_option(L.MHS_OPT_TINY_FIRST_ROWS, -1)
+        A = synth.SYNTH["mac_econ_fwd500"]()
+        check(t2, A, A)
+        assert t2.stat("nft") == 0
+        A.d_release_csr()
+    finally:
+        t2.close()
+
+
+def test_nft_slots_skipped_under_memory_budget(tool):
+    """the probe-less numeric-first slots (M * 128 * 12 bytes) are left out when they do
+    not fit the context's memory budget -- the call runs without them instead of chunking."""
+    from mhspgemm import _lib as L
+    A = synth.SYNTH["mac_econ_fwd500"]()  # slots 206 500 * 1536 B = 317 MB; workspace ~350 MB, C 59 MB
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        t2.set_option(L.MHS_OPT_MEM_BUDGET, 520)
+        check(t2, A, A)
+        assert t2.stat("nft") == 0 and t2.chunked_calls() == 0
+        A.d_release_csr()
+    finally:
+        t2.close()

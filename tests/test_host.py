@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.lib_path()], capture_output=True, text=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert set(names) <= exported
-    assert L.mhs_abi_version() == 9
+    assert L.mhs_abi_version() == 10
 
 
 def test_vendor_library_exports_every_declared_symbol():

@@ -1,0 +1,39 @@
+#!/bin/bash
+# One parametrised GPU driver (replaces the per-round tools/r05_*.sh scratch scripts).
+#   tools/gpu.sh check <tag> [pytest -k expr]     GPU suite, smoke, default bench line
+#   tools/gpu.sh ab <tag> "<matrices>" "<ENV=..>|<ENV=..>" [reps]
+#                                                  pipelined steps (tools/pipe.py) per env variant,
+#                                                  two interleaved rounds; "-" = the default env
+#   tools/gpu.sh bench <tag> [bench.py args]      one bench.py line
+#   tools/gpu.sh prof <tag> <matrix> [passes]     rocprofv3 kernel stats + FETCH/WRITE passes of
+#                                                  bench.py --matrix <matrix> (tools/bench_profile.sh)
+# Every GPU step runs under its own timeout; the first failure ends the script.
+set -o pipefail
+export TMPDIR=/tmp MHS_SYNTH_CACHE=/tmp/mhs_synth
+mode=$1; tag=$2; out=gpurun_out/$tag; mkdir -p $out
+case $mode in
+check)
+  bash tools/gpu_check.sh $tag "$3" || exit 1 ;;
+ab)
+  mats=$3; IFS='|' read -ra vars <<< "$4"; reps=${5:-3}
+  for r in 1 2; do
+    i=0
+    for v in "${vars[@]}"; do
+      envs=(); [ "$v" != "-" ] && read -ra envs <<< "$v"
+      env "${envs[@]}" timeout -k 10 400 python tools/pipe.py $mats --reps $reps > $out/v${i}_$r.jsonl 2>> $out/err.log \
+        || { tail -20 $out/err.log; exit 1; }
+      i=$((i+1))
+    done
+  done
+  python3 tools/pipe_table.py $out "$4" | tee $out/table.txt ;;
+bench)
+  shift 2
+  timeout -k 10 600 python bench.py "$@" > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
+  cut -c1-3000 $out/bench.json ;;
+prof)
+  bash tools/bench_profile.sh $tag "$3" "$4" > $out/prof.log 2>&1 || { tail -20 $out/prof.log; exit 1; }
+  tail -8 $out/prof.log ;;
+*)
+  echo "usage: tools/gpu.sh check|ab|bench|prof <tag> ..."; exit 2 ;;
+esac
+echo GPUDONE $mode $tag
