@@ -95,6 +95,8 @@ struct mhs_ctx {
     Stats plan_h{};
     long long gen = 0;        // bumped by every mhs_ctx_set_option (options change the pipeline)
     int* d_go = nullptr;      // k_scan's verdict on a speculated plan (device int)
+    int spec_nss = 1;         // streams of a speculated numeric phase (MHS_SPEC_NSS): the aux streams'
+                              // waits on a fork event that has not completed yet cost more than the overlap
 };
 
 namespace {
@@ -386,6 +388,13 @@ constexpr int NUM_GLOBAL_GRID = 128;
 #define MHS_SPLIT_FLOP_LOG2 24  // block bins split by LDS need from 2^this products on
 #endif
 
+// Streams the numeric launches of `h` are dealt over: several heavy bins go over the aux
+// streams (fork/join costs ~10-20 us, so only for at least 3 launches of a product worth it).
+int numeric_streams(const mhs_ctx* ctx, const Stats& h) {
+    const int nl = numeric_launches(h);
+    return (nl >= 3 && h.flop >= (1ull << MHS_MULTI_FLOP_LOG2)) ? std::min(ctx->num_streams, nl) : 1;
+}
+
 // The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
 // the aux streams, which join the call's stream again.
 int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out) {
@@ -393,8 +402,8 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     // several heavy bins: deal them over the aux streams (fork/join costs ~10-20 us,
     // so only when there are at least 3 launches of a product worth it)
     hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
-    const int nl = numeric_launches(h);
-    const int nss = (nl >= 3 && h.flop >= (1ull << MHS_MULTI_FLOP_LOG2)) ? std::min(ctx->num_streams, nl) : 1;
+    int nss = numeric_streams(ctx, h);
+    if (w.go) nss = std::min(nss, ctx->spec_nss);  // speculated: the fork event is still pending (see spec_nss)
     hipError_t fe = hipSuccess;
     if (nss > 1) {
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
@@ -404,6 +413,7 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     // numeric launch has gone out on the call's stream (launch_numeric)
     auto fork = [&]() {
         for (int i = 1; i < nss && fe == hipSuccess; ++i) fe = hipStreamWaitEvent(ss[i], ctx->fork_ev, 0);
+        return fe == hipSuccess;
     };
     // block bins split by LDS need only where their two launches can run side by side (on
     // one stream the hub rows' launch would no longer overlap the others' bulk).  The partition
@@ -418,14 +428,15 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     ctx->stat[MHS_STAT_MULTI_STREAM] += nss > 1;
     const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
                                     ctx->dense_span_max, split, split ? ctx->split_ev : nullptr,
-                                    nss > 1 ? std::function<void()>(fork) : std::function<void()>());
-    MHS_HIP(fe);
-    MHS_HIP(hipGetLastError());
+                                    nss > 1 ? std::function<bool()>(fork) : std::function<bool()>());
+    // joins first: an error below must not leave aux-stream work behind the call's stream
     for (int i = 1; i < nss; ++i)
         if (used & (1 << i)) {
             MHS_HIP(hipEventRecord(ctx->join_ev[i - 1], ss[i]));
             MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[i - 1], 0));
         }
+    MHS_HIP(fe);
+    MHS_HIP(hipGetLastError());
     return MHS_OK;
 }
 
@@ -638,6 +649,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     if (const char* e = getenv("MHS_NFT_AUTO_AVG")) ctx->nft_auto_avg = atoi(e);
     if (const char* e = getenv("MHS_NO_SPEC")) ctx->spec = atoi(e) == 0;
+    if (const char* e = getenv("MHS_SPEC_NSS")) ctx->spec_nss = std::max(1, std::min(atoi(e), mhs_ctx::NAUX + 1));
     *out = ctx;
     return MHS_OK;
 }
@@ -853,7 +865,11 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         key.mc_list = mc_list;
     }
     const bool plannable = ctx->spec && M > 0 && !probe && !fork_sym;
-    const bool spec = plannable && ctx->plan_valid && ctx->plan_key == key;
+    // (only plans whose numeric phase runs on one stream: dealt over the aux streams, the launches
+    // would wait on a fork event k_scan has not reached yet, and those waits measured slower than
+    // the hand-off they save -- scircuit-like +3..18 %, cop20k-like +7 %; r06b)
+    const bool spec = plannable && ctx->plan_valid && ctx->plan_key == key &&
+                      std::min(numeric_streams(ctx, ctx->plan_h), ctx->spec_nss) == numeric_streams(ctx, ctx->plan_h);
     const Stats ph = ctx->plan_h;  // (a copy: this call replaces the plan)
     ctx->plan_valid = false;  // (set again by this call's success)
     // ---- Calculate_C_nnz ------------------------------------------------------------

@@ -4565,7 +4565,7 @@ struct NumLaunch {
 
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
                    double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max, bool split,
-                   hipEvent_t split_ev, const std::function<void()>& fork) {
+                   hipEvent_t split_ev, const std::function<bool()>& fork) {
     std::vector<NumLaunch> L;
     auto add = [&](std::function<void(hipStream_t)> go) { L.push_back(NumLaunch{std::move(go)}); };
     NumArgs a{};
@@ -4795,15 +4795,17 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     // aux streams' waits on the fork event are set up after it (`fork`, host API calls that would
     // otherwise sit between the hand-off and the first numeric kernel: round 5, scircuit-like's
     // hand-off gap 46 -> ? us)
+    // (a failed fork -- the aux streams' wait on the fork event -- sends every later launch to
+    // ss[0]: no aux-stream launch may run without its dependency on the pre-numeric work)
     int used = 0;
-    const int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
+    int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
     for (size_t i = 0; i < L.size(); ++i) {
+        if (i == 1 && n > 1 && fork && !fork()) n = 1;
         const int k = n > 1 ? (int)(i % n) : 0;
-        if (i == 1 && n > 1 && fork) fork();
         used |= 1 << k;
         L[i].go(ss[k]);
     }
-    if (L.size() <= 1 && n > 1 && fork) fork();  // (the caller's joins expect the fork)
+    if (L.size() <= 1 && n > 1 && fork) (void)fork();  // (the caller's error check expects the fork)
     return used;
 }
 }  // namespace mhs

@@ -357,6 +357,13 @@ class ShardPlan:
         self.ranges = rng[:, :2]
         self.rowlen = (blk.ptr[1:] - blk.ptr[:-1]).to(torch.int32)
         nrow, nnz = blk.r1 - blk.r0, blk.col.numel()
+        # B = A is held as the ranks' row blocks: they must tile [0, M_global) in rank order (the full
+        # mode stacks them as B and reads A's global columns as local B ids; the halo mode finds a
+        # row's owner by searching the range starts).  Every rank sees the same ranges, so either
+        # all raise or none (the check had gone with the round-5 full-mode rewrite)
+        if not (rng[0, 0] == 0 and rng[-1, 1] == M_global and all(rng[:, 1] >= rng[:, 0]) and
+                all(rng[q, 1] == rng[q + 1, 0] for q in range(P - 1))):
+            raise ValueError("ShardPlan: the ranks' row blocks must tile [0, M) in rank order")
         if mode == "full":
             # every peer gets this rank's whole block; this rank gets every block
             self.srows = [nrow] * P

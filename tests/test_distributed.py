@@ -82,7 +82,7 @@ def _worker(rank, world, port, q):
         q.put({"rank": rank, "error": traceback.format_exc()})
 
 
-def _planned_worker(rank, world, port, q, mode):
+def _planned_worker(rank, world, port, q, mode, order="ranked"):
     try:
         sys.path[:0] = [str(ROOT), str(ROOT / "mh-spgemm_amd"), str(ROOT / "tests")]
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -96,7 +96,19 @@ def _planned_worker(rank, world, port, q, mode):
         M, ptr, col, val = _banded(M=900)
         rf = D.row_flop(ptr, col, ptr)
         bnd = D.partition_rows(rf, world)
-        blk = D.local_block(ptr, col, val, int(bnd[rank]), int(bnd[rank + 1]), "cpu")
+        q_ = world - 1 - rank if order == "reversed" else rank  # "reversed": ranges not in rank order
+        blk = D.local_block(ptr, col, val, int(bnd[q_]), int(bnd[q_ + 1]), "cpu")
+        if order == "gap":  # rank 0 owns no rows at the front: not a tiling
+            blk = D.local_block(ptr, col, val, int(bnd[q_]) + (5 if rank == 0 else 0), int(bnd[q_ + 1]), "cpu")
+        if order != "ranked":  # blocks that do not tile [0, M) in rank order are refused on every rank
+            try:
+                D.ShardPlan(blk, M, mode=mode)
+                ok = False
+            except ValueError:
+                ok = True
+            dist.destroy_process_group()
+            q.put({"rank": rank, "ok_b": ok, "ok_c": ok, "nB": 0})
+            return
         plan = D.ShardPlan(blk, M, mode=mode)
         # the local B holds exactly the planned rows of the global matrix
         Bp, Bc, Bv = plan.exchange()
@@ -139,12 +151,14 @@ def _banded(M=900, width=40, per=8, seed=4):
     return M, ptr.astype(np.int32), c, rng.uniform(0.1, 1.0, len(c))
 
 
-@pytest.mark.parametrize("world,mode", [(2, "halo"), (3, "halo"), (3, "full"), (4, "halo"), (4, "full")])
-def test_planned_exchange_gloo(world, mode):
+@pytest.mark.parametrize("world,mode,order", [(2, "halo", "ranked"), (3, "halo", "ranked"), (3, "full", "ranked"),
+                                              (4, "halo", "ranked"), (4, "full", "ranked"), (3, "full", "reversed"),
+                                              (3, "full", "gap")])
+def test_planned_exchange_gloo(world, mode, order):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_planned_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    procs = [ctx.Process(target=_planned_worker, args=(r, world, port, q, mode, order)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in range(world)]

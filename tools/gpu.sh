@@ -5,6 +5,7 @@
 #                                                  pipelined steps (tools/pipe.py) per env variant,
 #                                                  two interleaved rounds; "-" = the default env
 #   tools/gpu.sh bench <tag> [bench.py args]      one bench.py line
+#   tools/gpu.sh trace <tag> "<matrices>" ["ENV=.."]  kernel timelines of pipelined steps (rocprofv3)
 #   tools/gpu.sh prof <tag> <matrix> [passes]     rocprofv3 kernel stats + FETCH/WRITE passes of
 #                                                  bench.py --matrix <matrix> (tools/bench_profile.sh)
 # Every GPU step runs under its own timeout; the first failure ends the script.
@@ -30,6 +31,15 @@ bench)
   shift 2
   timeout -k 10 600 python bench.py "$@" > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
   cut -c1-3000 $out/bench.json ;;
+trace)
+  # kernel timelines of pipelined steps: tools/gpu.sh trace <tag> "<matrices>" ["ENV=.. ENV=.."]
+  envs=(); [ -n "$4" ] && read -ra envs <<< "$4"
+  for m in $3; do
+    env "${envs[@]}" timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $out/$m -o run -- python3 tools/pipe.py $m --reps 1 --steps 10 > $out/$m.log 2>&1 \
+      || { echo "trace $m failed"; tail -5 $out/$m.log; exit 1; }
+    python3 tools/timeline.py "$(find $out/$m -name '*kernel_trace.csv' | head -1)" > $out/$m/timeline.txt 2>&1
+    echo "== $m $4"; cat $out/$m/timeline.txt
+  done ;;
 prof)
   bash tools/bench_profile.sh $tag "$3" "$4" > $out/prof.log 2>&1 || { tail -20 $out/prof.log; exit 1; }
   tail -8 $out/prof.log ;;
