@@ -358,6 +358,10 @@ def main():
                     "frac_e2e": round(bcm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                     "_frac_e2e": bcm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                     "suitesparse_stats": synth.TARGETS.get(m),
+                    # the stand-in's deviation from them (say how close each stand-in is)
+                    "standin_vs_suitesparse": ({k: round(synth.ACHIEVED[m][k] / v - 1, 3)
+                                                for k, v in synth.TARGETS[m].items() if k in synth.ACHIEVED.get(m, {})}
+                                               if src_m.startswith("synthetic") and m in synth.TARGETS else None),
                     "phases_ms": {k: round(getattr(tm, k), 4) for k in (
                         "Form_mask_matrix_B", "symbolic_binning", "Calculate_C_nnz", "numeric_binning", "Numeric",
                         "total_e2e")},

@@ -234,16 +234,23 @@ def test_mtx_cache_env_words(tmp_path, monkeypatch):
     assert not (tmp_path / "false").exists() and not (tmp_path / "m.mtx.mhscsr").exists()
 
 
-@pytest.mark.parametrize("name", ["webbase-1M", "cop20k_A"])
+@pytest.mark.parametrize("name", ["cant", "webbase-1M", "mac_econ_fwd500", "scircuit", "cop20k_A", "cage15"])
 def test_standin_stats(name):
-    """the stand-ins recalibrated to SURVEY §8's SuiteSparse statistics --
-    the counts synth.ACHIEVED records hold, and they are within 20 % of synth.TARGETS."""
+    """every BASELINE config's stand-in against SURVEY §8's
+    SuiteSparse statistics -- the counts synth.ACHIEVED records hold (nnz(C) recounted by the
+    oracle below 2 M rows; cage15-like's 9.3e8 by tools/standin_stats.py), and each is within its
+    synth.CALIBRATED_TOL of synth.TARGETS."""
     from mhspgemm import synth
     A = synth.SYNTH[name]()
     bl = np.diff(A.ptr).astype(np.int64)
     got = dict(M=A.M, nnzA=A.nnz, flop=int(bl[A.col].sum()), max_row=int(bl.max()))
     rec, tgt = synth.ACHIEVED[name], synth.TARGETS[name]
     for k, v in got.items():
-        assert v == rec[k], (k, v, rec[k])
+        assert k not in rec or v == rec[k], (k, v, rec[k])
+    if A.M < 2_000_000:
+        Cp, _, _ = orc.spgemm(A.ptr, A.col, A.val, A.ptr, A.col, A.val, A.N)
+        assert int(Cp[-1]) == rec["nnzC"]
+    tol = synth.CALIBRATED_TOL[name]
     for k in ("nnzA", "flop", "nnzC", "max_row"):
-        assert abs(rec[k] / tgt[k] - 1) <= 0.2, (k, rec[k], tgt[k])
+        if k in tgt:
+            assert abs(rec[k] / tgt[k] - 1) <= tol, (k, rec[k], tgt[k])
