@@ -80,6 +80,30 @@ __device__ unsigned long long* g_rowdiag;  // [M][8]
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
         if (tm.rank() == 0) g_rowdiag[(size_t)row * 8 + (k)] = t_ - tp_; \
         tp_ = t_;                                                       \
+        MHS_FLIGHT_PHASE(k);                                            \
+    } while (0)
+// Flight recorder (stamps builds, round 6): every wave of the numeric wave kernels writes, to
+// fine-grained host memory, the row it is on, its list index, the last phase stamp it passed
+// and a tick.  The host reads it while the kernels run (tools/diag/flight.py): a wave that
+// never finishes shows where it is.  Plain system-scope vector stores; off unless set up.
+__device__ unsigned long long* g_flight;  // [wave][4]: row | li << 32, phase, tick, calls
+extern "C" int mhs_diag_flight(void* dev_ptr) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_flight), &dev_ptr, sizeof(void*));
+}
+__device__ __forceinline__ void flight_put(int slot, unsigned long long v) {
+    unsigned long long* f = g_flight;
+    if (!f) return;
+    const long long w = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w < 65536 && (threadIdx.x & 63) == 0)
+        __hip_atomic_store(f + w * 4 + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define MHS_FLIGHT_PHASE(k) flight_put(1, (unsigned long long)(k) + 1)
+#define MHS_FLIGHT_TAKE(li) flight_put(3, (unsigned long long)(unsigned)(li))
+#define MHS_FLIGHT_ROW(row, li)                                                      \
+    do {                                                                             \
+        flight_put(0, (unsigned long long)(unsigned)(row) | ((unsigned long long)(unsigned)(li) << 32)); \
+        flight_put(1, 0ull);                                                         \
+        flight_put(2, __builtin_amdgcn_s_memtime());                                 \
     } while (0)
 extern "C" int mhs_diag_setup(int M, unsigned long long** dev) {
     hipError_t e = hipMalloc((void**)dev, (size_t)M * 64);
@@ -107,6 +131,8 @@ extern "C" int mhs_diag_setup_sym(int M, unsigned long long** dev) {
 #define MHS_STAMP(k)
 #define MHS_SSTAMP0()
 #define MHS_SSTAMP(k)
+#define MHS_FLIGHT_ROW(row, li)
+#define MHS_FLIGHT_TAKE(li)
 #endif
 // (bisecting the round-4/5 stamps hang on cage15-like: MHS_STAMP_NUM_BODY=0 keeps the stamps out
 // of num_row_body, the wave and 256-thread rows)
@@ -3707,6 +3733,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
     WaveTeam tm;
     auto one = [&](int li) {
         const int row = __builtin_amdgcn_readfirstlane(a.list[li]);
+        MHS_FLIGHT_ROW(row, li);
         if constexpr (GROUPED)  // a group head: R rows of one pattern
             num_row<WaveTeam, false, true, MODES_ALL, O32>(tm, a, row, reg + WAVE_HDR, (int*)reg, nullptr,
                                                          __builtin_amdgcn_readfirstlane((int)a.grp[row]) & GRP_RMASK);
@@ -3739,6 +3766,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
             int t = 0;
             if (lane_id() == 0) t = atomicAdd(cur, 1);
             const int li = split + __builtin_amdgcn_readfirstlane(t);
+            MHS_FLIGHT_TAKE(li);
             if (li >= end) break;
             one(li);
         }

@@ -1,12 +1,15 @@
 #!/bin/bash
-# Diagnostic library: per-row, per-phase s_memtime stamps of the numeric rows
-# (-DMHS_ROW_STAMPS=1; read by tools/diag/stamps*.py).  Built into tools/diag/v9.
+# Diagnostic library: per-row, per-phase s_memtime stamps of the numeric rows and the flight
+# recorder (-DMHS_ROW_STAMPS=1; read by tools/diag/stamps2.py and tools/diag/flight.py), built
+# into tools/diag/stamps/ (git-ignored; travels to the GPU box).  Extra -D flags: "$@".
 set -e
 cd "$(dirname "$0")"
-SRC=../../mh-spgemm_amd/csrc
-mkdir -p v9
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -DMHS_ROW_STAMPS=1 -c $SRC/mhs_kernels.hip -o v9/k.o
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -x hip -c $SRC/mhs_api.cpp -o api.o
-[ tr.o -nt $SRC/mhs_transpose.hip ] || hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c $SRC/mhs_transpose.hip -o tr.o
-hipcc -O3 -std=c++17 -fPIC -c $SRC/mhs_mmio.cpp -o mmio.o
-hipcc --offload-arch=gfx950 -shared -fPIC -o v9/libmhspgemm.so v9/k.o tr.o api.o mmio.o -lpthread
+ROOT=$(cd ../.. && pwd)
+SRC=$ROOT/mh-spgemm_amd/csrc
+B=$ROOT/mh-spgemm_amd/build
+make -s -C $ROOT/mh-spgemm_amd ARCH=gfx950 lib
+mkdir -p stamps
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include -DMHS_ROW_STAMPS=1 "$@" -c $SRC/mhs_kernels.hip -o stamps/k.o
+hipcc --offload-arch=gfx950 -shared -fPIC -o stamps/libmhspgemm.so stamps/k.o $B/mhs_transpose.o $B/mhs_hbm.o $B/mhs_api.o $B/mhs_mmio.o -lpthread
+rm -f stamps/k.o
+echo built tools/diag/stamps/libmhspgemm.so
