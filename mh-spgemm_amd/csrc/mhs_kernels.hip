@@ -82,6 +82,9 @@ __device__ unsigned long long* g_rowdiag;  // [M][8]
         tp_ = t_;                                                       \
         MHS_FLIGHT_PHASE(k);                                            \
     } while (0)
+#ifndef MHS_FLIGHT
+#define MHS_FLIGHT 1  // the flight recorder in stamps builds (0: compiled out)
+#endif
 // Flight recorder (stamps builds, round 6): every wave of the numeric wave kernels writes, to
 // fine-grained host memory, the row it is on, its list index, the last phase stamp it passed
 // and a tick.  The host reads it while the kernels run (tools/diag/flight.py): a wave that
@@ -91,6 +94,7 @@ extern "C" int mhs_diag_flight(void* dev_ptr) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_flight), &dev_ptr, sizeof(void*));
 }
 __device__ __forceinline__ void flight_put(int slot, unsigned long long v) {
+    if (!MHS_FLIGHT) return;
     unsigned long long* f = g_flight;
     if (!f) return;
     const long long w = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -110,6 +114,10 @@ extern "C" int mhs_diag_setup(int M, unsigned long long** dev) {
     if (e == hipSuccess) e = hipMemset(*dev, 0, (size_t)M * 64);
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_rowdiag), dev, sizeof(void*));
     return (int)e;
+}
+// the row stamps into a caller's buffer (e.g. fine-grained host memory, read while a kernel runs)
+extern "C" int mhs_diag_set_rows(void* dev_ptr) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rowdiag), &dev_ptr, sizeof(void*));
 }
 // symbolic rows (sym_row_s): [M][4] phases -- clear, tile walk, count, row cache / spill list
 __device__ unsigned long long* g_symdiag;

@@ -8,8 +8,9 @@ ROOT=$(cd ../.. && pwd)
 SRC=$ROOT/mh-spgemm_amd/csrc
 B=$ROOT/mh-spgemm_amd/build
 make -s -C $ROOT/mh-spgemm_amd ARCH=gfx950 lib
-mkdir -p stamps
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include -DMHS_ROW_STAMPS=1 "$@" -c $SRC/mhs_kernels.hip -o stamps/k.o
-hipcc --offload-arch=gfx950 -shared -fPIC -o stamps/libmhspgemm.so stamps/k.o $B/mhs_transpose.o $B/mhs_hbm.o $B/mhs_api.o $B/mhs_mmio.o -lpthread
-rm -f stamps/k.o
-echo built tools/diag/stamps/libmhspgemm.so
+OUT=${OUT:-stamps}
+mkdir -p $OUT
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include -DMHS_ROW_STAMPS=1 "$@" -c $SRC/mhs_kernels.hip -o $OUT/k.o
+hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libmhspgemm.so $OUT/k.o $B/mhs_transpose.o $B/mhs_hbm.o $B/mhs_api.o $B/mhs_mmio.o -lpthread
+rm -f $OUT/k.o
+echo built tools/diag/$OUT/libmhspgemm.so

@@ -36,6 +36,16 @@ assert hip.hipHostGetDevicePointer(ctypes.byref(dptr), host, ctypes.c_uint(0)) =
 L.mhs_diag_flight.argtypes = [ctypes.c_void_p]
 assert L.mhs_diag_flight(dptr) == 0
 fl = np.ctypeslib.as_array(ctypes.cast(host, ctypes.POINTER(ctypes.c_uint64)), shape=(NW, 4))
+rows_h = None
+if os.environ.get("FLIGHT_HOST_ROWS"):  # the row stamps themselves in host memory (no extra code)
+    rh = ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(rh), ctypes.c_size_t(A.M * 64), ctypes.c_uint(0x2 | 0x40000000)) == 0
+    ctypes.memset(rh, 0, A.M * 64)
+    rd = ctypes.c_void_p()
+    assert hip.hipHostGetDevicePointer(ctypes.byref(rd), rh, ctypes.c_uint(0)) == 0
+    L.mhs_diag_set_rows.argtypes = [ctypes.c_void_p]
+    assert L.mhs_diag_set_rows(rd) == 0
+    rows_h = np.ctypeslib.as_array(ctypes.cast(rh, ctypes.POINTER(ctypes.c_uint64)), shape=(A.M, 8))
 done = []
 
 
@@ -72,5 +82,15 @@ for w in np.nonzero(inrow)[0][:40]:
     print(f"  wave {w}: row {row} li {li} phase {int(snap[w, 1]) - 1} last take {int(snap[w, 3])} "
           f"tick {int(snap[w, 2])} moving {bool(moving[w])} | nA {int(nA[row]) if row < A.M else -1} flop {flop} "
           f"A-span tiles {span}", flush=True)
+if rows_h is not None:
+    st = rows_h[:, :6].copy()
+    started = (st != 0).any(1)
+    part = started & ~(st != 0).all(1)
+    print(f"ROWS: started {started.sum()} of {A.M}, partial {part.sum()}", flush=True)
+    for r in np.nonzero(part)[0][:40]:
+        cols = A.col[A.ptr[r]:A.ptr[r + 1]]
+        flop = int(blen[cols].sum()) if len(cols) else 0
+        span = (int(cols.max() >> 6) - int(cols.min() >> 6) + 1) if len(cols) else 0
+        print(f"  row {r}: stamps {[int(x) for x in st[r]]} nA {int(nA[r])} flop {flop} A-span tiles {span}", flush=True)
 print("FLIGHT: exiting with the kernel still running", flush=True)
 os._exit(3)
