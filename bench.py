@@ -530,6 +530,13 @@ def main():
         if "copy_GBps" in hbm:
             out["roofline"]["peak_measured_copy"] = hbm["copy_GBps"]
             out["roofline"]["frac_vs_measured_copy"] = round(achieved / hbm["copy_GBps"], 4)
+            #  the launch priced against the measured read and write peaks for its
+            # own mix: compulsory reads (A's arrays, C.ptr) at the read peak plus compulsory writes
+            # (C.col / C.val) at the write peak, over its measured duration
+            rd, wr = 8 * (M_glob + 1) + 12 * nnzA, 12 * nnzC
+            if hbm.get("read_GBps") and hbm.get("write_GBps"):
+                t_ideal = rd / (hbm["read_GBps"] * 1e9) + wr / (hbm["write_GBps"] * 1e9)
+                out["roofline"]["frac_vs_measured_read_write"] = round(t_ideal / (avg_num * 1e-3), 4)
         out["hbm_peak"] = dict(hbm, spec_GBps=HBM_PEAK_GBPS,
                                kernels="mhs_hbm_peak: the best of 38 kernel shapes per kind (16 B a lane, 2-16 accesses in flight, grid-stride or one slab per block, 1-32 blocks per CU, cached or nontemporal) and the runtime's own D2D copy / fill, 2 GiB buffers")
         if configs:

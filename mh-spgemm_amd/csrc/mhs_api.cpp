@@ -397,7 +397,8 @@ int numeric_streams(const mhs_ctx* ctx, const Stats& h) {
 
 // The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
 // the aux streams, which join the call's stream again.
-int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out) {
+int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out,
+                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
     hipStream_t s = ctx->stream;
     // several heavy bins: deal them over the aux streams (fork/join costs ~10-20 us,
     // so only when there are at least 3 launches of a product worth it)
@@ -405,6 +406,7 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     int nss = numeric_streams(ctx, h);
     if (w.go) nss = std::min(nss, ctx->spec_nss);  // speculated: the fork event is still pending (see spec_nss)
     hipError_t fe = hipSuccess;
+    if (nss > 1 && ev0) MHS_HIP(hipEventRecord(ev0, s));  // (several streams: events of their own)
     if (nss > 1) {
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         for (int i = 1; i < nss; ++i) ss[i] = ctx->aux[i - 1];
@@ -428,13 +430,19 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     ctx->stat[MHS_STAT_MULTI_STREAM] += nss > 1;
     const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
                                     ctx->dense_span_max, split, split ? ctx->split_ev : nullptr,
-                                    nss > 1 ? std::function<bool()>(fork) : std::function<bool()>());
+                                    nss > 1 ? std::function<bool()>(fork) : std::function<bool()>(),
+                                    nss == 1 ? ev0 : nullptr, nss == 1 ? ev1 : nullptr);
+    if (nss == 1 && (used & (1 << 30))) {  // (no launch carried them)
+        if (ev0) MHS_HIP(hipEventRecord(ev0, s));
+        if (ev1) MHS_HIP(hipEventRecord(ev1, s));
+    }
     // joins first: an error below must not leave aux-stream work behind the call's stream
     for (int i = 1; i < nss; ++i)
         if (used & (1 << i)) {
             MHS_HIP(hipEventRecord(ctx->join_ev[i - 1], ss[i]));
             MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[i - 1], 0));
         }
+    if (nss > 1 && ev1) MHS_HIP(hipEventRecord(ev1, s));
     MHS_HIP(fe);
     MHS_HIP(hipGetLastError());
     return MHS_OK;
@@ -928,18 +936,20 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
                 }
                 t_malloc = ms_since(T5);
                 if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
-                if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
                 w.go = ctx->d_go;
                 if (ph.nnzC > 0) {
                     out.nnz = (int)ph.nnzC;
-                    rc = run_numeric(ctx, a, b, w, ph, out);
+                    rc = run_numeric(ctx, a, b, w, ph, out, nring ? ctx->nev[2 * slot] : nullptr,
+                                     nring ? ctx->nev[2 * slot + 1] : nullptr);
                     if (rc) {
                         (void)hipStreamSynchronize(s);
                         mhs_ctx_recycle(ctx, &out);
                         return rc;
                     }
+                } else if (nring) {
+                    MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
+                    MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
                 }
-                if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
                 if (timed) MHS_HIP(hipEventRecord(ctx->ev[6], s));
                 launched = true;
                 ++ctx->stat[MHS_STAT_SPEC];
@@ -1015,17 +1025,19 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
 
         // ---- Numeric -------------------------------------------------------------------------
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[5], s));
-        if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
         w.go = nullptr;
         if (out.nnz > 0) {
-            rc = run_numeric(ctx, a, b, w, h, out);
+            rc = run_numeric(ctx, a, b, w, h, out, nring ? ctx->nev[2 * slot] : nullptr,
+                             nring ? ctx->nev[2 * slot + 1] : nullptr);
             if (rc) {
                 mhs_ctx_recycle(ctx, &out);
                 return rc;
             }
+        } else if (nring) {
+            MHS_HIP(hipEventRecord(ctx->nev[2 * slot], s));
+            MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
         }
         MHS_HIP(hipGetLastError());
-        if (nring) MHS_HIP(hipEventRecord(ctx->nev[2 * slot + 1], s));
         if (timed) MHS_HIP(hipEventRecord(ctx->ev[6], s));
     }
     ++ctx->ncalls;

@@ -451,10 +451,13 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
                           Published* pub, int seq, const SpecArgs& spec);
 // fork: called once before the first launch on an aux stream (the aux streams' waits on the
 // fork event; the first launch goes out on ss[0] before it); false: the waits failed, every
-// later launch goes to ss[0]
+// later launch goes to ss[0].  ev_start / ev_stop (optional): timing events carried by the first and
+// last dispatch of a single-stream phase; bit 30 of the result: not attached (several streams or
+// no launch) -- the caller records them
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
                    int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max,
-                   bool split, hipEvent_t split_ev = nullptr, const std::function<bool()>& fork = nullptr);
+                   bool split, hipEvent_t split_ev = nullptr, const std::function<bool()>& fork = nullptr,
+                   hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 // numeric launches a call makes for these bin counts (the 32-lane tiny classes share one; a
 // split block bin makes two)
 int numeric_launches(const Stats& h);

@@ -27,6 +27,8 @@
 // neighbouring rows (which share B rows) run on one XCD's L2.
 #include "mhs_internal.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <climits>
 #include <functional>
@@ -4332,10 +4334,25 @@ size_t sym_global_bytes_per_block(int N) {
     return (size_t)hash_slots(span_max) * 16;
 }
 
+// Numeric launches: the numeric-phase events (MHS_OPT_NUMERIC_EVENTS) ride on the first and last
+// dispatch packet of a single-stream numeric phase (hipExtLaunchKernel) instead of event records
+// of their own between the kernels -- each record measured ~5 us of idle before the next kernel
+// (pipelined cant-like steps, r06b timelines).  launch_numeric sets them for the launch at hand.
+namespace {
+thread_local hipEvent_t t_num_start = nullptr, t_num_stop = nullptr;
+}
+template <typename F, typename... Args>
+static void num_launch(F kernel, const dim3& g, const dim3& b, unsigned lds, hipStream_t s, Args... args) {
+    hipEvent_t e0 = t_num_start, e1 = t_num_stop;
+    t_num_start = t_num_stop = nullptr;
+    if (e0 || e1) hipExtLaunchKernelGGL(kernel, g, b, lds, s, e0, e1, 0u, args...);
+    else hipLaunchKernelGGL(kernel, g, b, lds, s, args...);
+}
+
 // Numeric tiny class c, `rows` rows.
 static void launch_tiny_num(int c, int rows, const TinyArgs& t, hipStream_t s) {
 #define MHS_TINY(WW, KK)                                                                                  \
-    hipLaunchKernelGGL((k_tiny_num<WW, KK>), dim3(round8((rows + 256 / (WW) - 1) / (256 / (WW)), MHS_TINY64_GRID)), \
+    num_launch((k_tiny_num<WW, KK>), dim3(round8((rows + 256 / (WW) - 1) / (256 / (WW)), MHS_TINY64_GRID)), \
                        dim3(256), 256 * (KK) * 8, s, t)
     switch (c) {
     case 0: MHS_TINY(tiny_w(0), tiny_k(0)); break;
@@ -4601,7 +4618,7 @@ struct NumLaunch {
 
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
                    double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max, bool split,
-                   hipEvent_t split_ev, const std::function<bool()>& fork) {
+                   hipEvent_t split_ev, const std::function<bool()>& fork, hipEvent_t ev_start, hipEvent_t ev_stop) {
     std::vector<NumLaunch> L;
     auto add = [&](std::function<void(hipStream_t)> go) { L.push_back(NumLaunch{std::move(go)}); };
     NumArgs a{};
@@ -4681,9 +4698,9 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             const int Lw = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
             const dim3 grid(round8((A.M + 256 / Lw - 1) / (256 / Lw), A.M >= MHS_NFT_BIG_M ? MHS_COPY_CAP_BIG : 16384));
             add([=](hipStream_t s) {
-                if (Lw == 4) hipLaunchKernelGGL(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
-                else if (Lw == 8) hipLaunchKernelGGL(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
-                else hipLaunchKernelGGL(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
+                if (Lw == 4) num_launch(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
+                else if (Lw == 8) num_launch(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
+                else num_launch(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
             });
         }
     }
@@ -4692,8 +4709,8 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         x.gbytes = align16(h.num_global_need);
         const int g = x.count < global_grid ? x.count : global_grid;
         add([=](hipStream_t s) {
-            if (o32) hipLaunchKernelGGL((k_num_block<1024, true, true>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
-            else hipLaunchKernelGGL((k_num_block<1024, true, false>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
+            if (o32) num_launch((k_num_block<1024, true, true>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
+            else num_launch((k_num_block<1024, true, false>), dim3(g), dim3(1024), BLOCK_HDR_1024, s, x);
         });
     }
     // block bins: rows past the bin's LDS split (hub rows) in a launch of their own, so the
@@ -4710,10 +4727,10 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             const hipStream_t s0 = ss[0];
             add([=](hipStream_t s) {
                 if (after && s != s0) (void)hipStreamWaitEvent(s, after, 0);  // (k_split_bins' lists)
-                if (T == 1024 && o32) hipLaunchKernelGGL((k_num_block<1024, false, true>), grid, dim3(1024), lds, s, x);
-                else if (T == 1024) hipLaunchKernelGGL((k_num_block<1024, false, false>), grid, dim3(1024), lds, s, x);
-                else if (o32) hipLaunchKernelGGL((k_num_block<256, false, true>), grid, dim3(256), lds, s, x);
-                else hipLaunchKernelGGL((k_num_block<256, false, false>), grid, dim3(256), lds, s, x);
+                if (T == 1024 && o32) num_launch((k_num_block<1024, false, true>), grid, dim3(1024), lds, s, x);
+                else if (T == 1024) num_launch((k_num_block<1024, false, false>), grid, dim3(1024), lds, s, x);
+                else if (o32) num_launch((k_num_block<256, false, true>), grid, dim3(256), lds, s, x);
+                else num_launch((k_num_block<256, false, false>), grid, dim3(256), lds, s, x);
             });
         };
         if (split && block_split_on(h, k)) {  // k_split_bins: small rows first, hub rows last
@@ -4732,24 +4749,24 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         x.qall = x.count <= MHS_DYN16_MAX;  // a few rows per resident wave: the launch's end is one heavy row
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_W16H_GRID));
         add([=](hipStream_t s) {
-            if (o32) hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES, true>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
-            else hipLaunchKernelGGL((k_num_wave_hash<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+            if (o32) num_launch((k_num_wave_hash<NUM_W16_BYTES, true>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+            else num_launch((k_num_wave_hash<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
         });
     }
     if (h.num_count[NUM_WSH] > 0) {
         const NumArgs x = wave_args(NUM_WSH);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, x.count >= MHS_NUM_WSH_BIG ? MHS_NUM_WSH_BIG_GRID : MHS_NUM_WSX_GRID));
         add([=](hipStream_t s) {
-            if (o32) hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
-            else hipLaunchKernelGGL((k_num_wave_hash<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+            if (o32) num_launch((k_num_wave_hash<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+            else num_launch((k_num_wave_hash<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
         });
     }
     if (h.num_count[NUM_W16] > 0) {
         const NumArgs x = wave_args(NUM_W16);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, 2048));
         add([=](hipStream_t s) {
-            if (o32) hipLaunchKernelGGL((k_num_wave_direct<NUM_W16_BYTES, true>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
-            else hipLaunchKernelGGL((k_num_wave_direct<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+            if (o32) num_launch((k_num_wave_direct<NUM_W16_BYTES, true>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
+            else num_launch((k_num_wave_direct<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
         });
     }
     {
@@ -4791,7 +4808,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         if (f.nclass > 0) {
             t.list = w.bin_list;
             add([=](hipStream_t s) {
-                hipLaunchKernelGGL(k_tiny_num_small, dim3(f.blk0[f.nclass]), dim3(256), 256 * TINY_FUSED_KMAX * 8, s, t,
+                num_launch(k_tiny_num_small, dim3(f.blk0[f.nclass]), dim3(256), 256 * TINY_FUSED_KMAX * 8, s, t,
                                    f);
             });
         }
@@ -4806,8 +4823,8 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         x.wave_bytes = wave_region(h.num_wave_need[1], NUM_W16_BYTES);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, 2048));
         add([=](hipStream_t s) {
-            if (o32) hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true, false, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
-            else hipLaunchKernelGGL((k_num_wave<NUM_W16_BYTES, true, false, false>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+            if (o32) num_launch((k_num_wave<NUM_W16_BYTES, true, false, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+            else num_launch((k_num_wave<NUM_W16_BYTES, true, false, false>), grid, dim3(256), WPB * x.wave_bytes, s, x);
         });
     }
     if (h.num_count[NUM_WSG] > 0) {
@@ -4815,16 +4832,16 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
         x.wave_bytes = wave_region(h.num_wave_need[0], NUM_WSG_BYTES);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WS_GRID));
         add([=](hipStream_t s) {
-            if (o32) hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true, false, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
-            else hipLaunchKernelGGL((k_num_wave<NUM_WSG_BYTES, true, false, false>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+            if (o32) num_launch((k_num_wave<NUM_WSG_BYTES, true, false, true>), grid, dim3(256), WPB * x.wave_bytes, s, x);
+            else num_launch((k_num_wave<NUM_WSG_BYTES, true, false, false>), grid, dim3(256), WPB * x.wave_bytes, s, x);
         });
     }
     if (h.num_count[NUM_WS] > 0) {
         const NumArgs x = wave_args(NUM_WS);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, MHS_NUM_WSX_GRID));
         add([=](hipStream_t s) {
-            if (o32) hipLaunchKernelGGL((k_num_wave_direct<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
-            else hipLaunchKernelGGL((k_num_wave_direct<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+            if (o32) num_launch((k_num_wave_direct<NUM_WS_BYTES, true>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
+            else num_launch((k_num_wave_direct<NUM_WS_BYTES, false>), grid, dim3(256), WPB * NUM_WS_BYTES, s, x);
         });
     }
     // launch i on ss[i % n]: the first (largest rows) goes out on the call's stream at once, and the
@@ -4835,12 +4852,17 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     // ss[0]: no aux-stream launch may run without its dependency on the pre-numeric work)
     int used = 0;
     int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
+    const bool evs = n == 1 && !L.empty() && (ev_start || ev_stop);  // (single stream only: see num_launch)
     for (size_t i = 0; i < L.size(); ++i) {
         if (i == 1 && n > 1 && fork && !fork()) n = 1;
         const int k = n > 1 ? (int)(i % n) : 0;
         used |= 1 << k;
+        if (evs && i == 0) t_num_start = ev_start;
+        if (evs && i + 1 == L.size()) t_num_stop = ev_stop;
         L[i].go(ss[k]);
     }
+    t_num_start = t_num_stop = nullptr;
+    if (!evs && (ev_start || ev_stop)) used |= 1 << 30;  // the caller records the events itself
     if (L.size() <= 1 && n > 1 && fork) (void)fork();  // (the caller's error check expects the fork)
     return used;
 }
