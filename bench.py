@@ -553,7 +553,7 @@ def main():
         ph["t_ref_getTotal"] = round(float(np.mean([p.getTotal() for p in phases])), 4)
         ph["note"] = "5 synchronised calls with per-phase events, after the timed region"
         out["phases_ms"] = ph
-        out["bins"] = {"symbolic": phases[-1].sym_bins[:13], "numeric": phases[-1].num_bins[:16],
+        out["bins"] = {"symbolic": phases[-1].sym_bins[:12], "numeric": phases[-1].num_bins[:16],
                        "numeric_kernels": {NUM_BIN_KERNELS[i]: c for i, c in enumerate(phases[-1].num_bins[:16])
                                            if i and c}}
         if not args.no_cpu:

@@ -50,7 +50,6 @@ struct mhs_ctx {
     bool stats_zero = false; // the workspace's device Stats are zero (left so by the last k_scan)
     bool use_mcache = true;  // symbolic keeps narrow rows' tile masks for numeric (MHS_NO_MCACHE)
     bool tiny_num = true;    // numeric tiny (sort) classes (MHS_NO_TINY_NUM=1: off)
-    bool tile_sort = true;   // symbolic tile-sort class (SYM_TILE; MHS_NO_TILE_SORT=1: off)
     // numeric-first tiny rows from this many rows of A on (MHS_OPT_TINY_FIRST_ROWS,
     // MHS_NFT_MIN_M; < 0: never): one hand-off more per call, so big matrices only
     long long nft_min_m = 1 << 19;
@@ -328,8 +327,6 @@ Work make_work(mhs_ctx* ctx, const Layout& L, int M, long long nnzA, long long n
     w.spill.cap = L.spill_cap;
     w.tslot = (long long*)(ctx->ws + L.tslot);
     w.split_list = (int*)(ctx->ws + L.split_list);
-    // the symbolic tile-sort class: rows whose distinct tiles fit the row-cache list (MHS_NO_TILE_SORT=1: off)
-    w.tile_max = ctx->tile_sort ? (ctx->use_mcache ? std::min(TILE_SORT_MAX, mc_list) : TILE_SORT_MAX) : 0;
     if (L.near) {
         w.near_list = (int*)(ctx->ws + L.near_list);
         w.nsig = (unsigned*)(ctx->ws + L.nsig);
@@ -653,7 +650,6 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (getenv("MHS_NO_NEAR")) ctx->near = false;
     if (getenv("MHS_NO_SPLIT")) ctx->split = false;
     if (getenv("MHS_NO_TINY_NUM")) ctx->tiny_num = false;
-    if (const char* e = getenv("MHS_NO_TILE_SORT")) ctx->tile_sort = atoi(e) == 0;
     if (const char* e = getenv("MHS_NFT_MIN_M")) ctx->nft_min_m = atoll(e);
     if (getenv("MHS_NFT_NO_SLOTS")) ctx->nft_slots = false;
     if (const char* e = getenv("MHS_SYM_FORK")) ctx->sym_fork = atoi(e) != 0;

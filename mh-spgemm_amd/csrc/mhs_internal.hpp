@@ -38,7 +38,7 @@ constexpr int CURSOR_STRIDE = 16;  // ints
 constexpr int CURSOR_INTS = CURSOR_SLOTS * 8 * CURSOR_STRIDE;
 constexpr int SPILL_PARTS = 64;        // spill-list bump counters: cursor slots 32..39
 constexpr int SPILL_CURSOR_SLOT = 32;
-constexpr int BLOCK_BIG_SLOT = 29;     // cursors of the block bins' hub-row launches (29: 256, 30: 1024 threads)
+constexpr int BLOCK_BIG_SLOT = 28;     // cursors of the block bins' hub-row launches (28: 256, 29: 1024 threads)
 static_assert(SPILL_CURSOR_SLOT * 8 + SPILL_PARTS <= CURSOR_SLOTS * 8, "spill counters fit the cursor area");
 
 // Symbolic bins (by LDS need and tile work).
@@ -90,18 +90,8 @@ __host__ __device__ inline int tiny_class_sym(int flop, int nA) {
 enum SymBin : int {
     SYM_NONE = 0, SYM_WAVE = 1, SYM_B256 = 2, SYM_B1024 = 3, SYM_GLOBAL = 4, SYM_TINY = 5,
     SYM_WM = SYM_TINY + TINY_NC,  // wave per row with a 10 KiB table (scattered rows of a few hundred tiles)
-    SYM_TILE,                     // tile-sort class (round 6): see TILE_W below
     SYM_NB
 };
-// Symbolic tile-sort class (round 6): a row of at most TILE_W A entries and TILE_W * TILE_K tile
-// products (short rows over scattered tiles: cage15-, webbase-like) is counted by a team of TILE_W
-// lanes that sorts its (tile, mask) products in registers -- two rows a wave, no table -- ORs the
-// masks of equal tiles and leaves the row's distinct tiles as a key-sorted list in the row cache
-// (numeric then ranks them by a prefix sum in list order).  Rows of the small-table wave bin only.
-constexpr int TILE_W = 32, TILE_K = 4;
-constexpr int TILE_SORT_MAX = TILE_W * TILE_K;
-constexpr int TILE_EB = 7;  // sort key = (tile - row's first tile) << TILE_EB | element
-static_assert((1 << TILE_EB) == TILE_SORT_MAX, "element bits");
 // Numeric bins (by LDS need and product work).
 // NUM_WSG / NUM_W16G: row groups (up to RG_MAX consecutive rows of A with one
 // column pattern, processed together by one wave: every B value loaded feeds R rows).
@@ -439,7 +429,6 @@ struct Work {
     void* gscratch;    // global-bin scratch
     size_t gscratch_bytes;
     const int* go;     // speculated numeric launches: run only when *go == 1 (k_scan's verdict); nullptr: always
-    int tile_max;      // symbolic tile-sort class: rows of at most this many tile products (0: off)
 };
 
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);

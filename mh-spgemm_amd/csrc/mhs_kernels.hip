@@ -1150,11 +1150,8 @@ __device__ __forceinline__ void analyze_out(int row, long long flop, long long t
                                             int* __restrict__ ctiles, unsigned char* __restrict__ sym_bin,
                                             int* __restrict__ Cptr, unsigned char* __restrict__ asame,
                                             unsigned char* __restrict__ nft_bin, int& nslots, int& nother,
-                                            unsigned* __restrict__ nsig, int sort64_tile) {
+                                            unsigned* __restrict__ nsig, int sort64) {
     {
-        // sort64_tile: bit 0 = symbolic class 4 allowed, bits 8.. = the tile-sort class's tile-product cap
-        const bool sort64 = (sort64_tile & 1) != 0;
-        const int tile_max = sort64_tile >> 8;
         // a row with an out-of-range column enters no bin: the symbolic kernels gather
         // bmeta[Acol[j]] unchecked, and the host returns MHS_ERR_INVALID before numeric
         asame[row] = (unsigned char)((differ || bad) ? 0 : 1);
@@ -1168,20 +1165,14 @@ __device__ __forceinline__ void analyze_out(int row, long long flop, long long t
         // so no numeric table kernel looks for masks symbolic did not keep)
         const int tc = sort64 && (long long)span * TILE_BITS - 1 <= TINY_NUM_NMAX ? sym_tiny_class(f, nA, tf, span)
                                                                                    : tiny_class_sym(f, nA);
-        const int bin0 = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
-        // the tile-sort class: small-table wave rows of <= TILE_W entries and few tile products that
-        // numeric reads as a row-cache list (not the narrow rows' dense masks); keys hold the tile
-        // relative to the row's first in 25 bits
-        const bool tsort = bin0 == SYM_WAVE && tile_max > 0 && nA <= TILE_W && tf <= tile_max && !mcached(span, tf) &&
-                           span < (1 << 25);
-        const int bin = tsort ? SYM_TILE : bin0;
+        const int bin = tc >= 0 ? SYM_TINY + tc : sym_bin_of(f, tf, span);
         sym_bin[row] = (unsigned char)bin;
         // near row-group signature (k_bin_list links rows whose signatures match: the same
         // C tile span and first A column, both in the small-table wave bin); a collision only
         // adds a candidate that k_sym_rare's check turns down (it compares every row's span,
         // counts and row-cache words with the head's)
         if (nsig)
-            nsig[row] = (bin0 == SYM_WAVE && nA >= 8 && !bad)
+            nsig[row] = (bin == SYM_WAVE && nA >= 8 && !bad)
                             ? (((unsigned)lo * 0x9E3779B1u) ^ ((unsigned)hi * 0x85EBCA77u) ^
                                ((unsigned)kfirst * 0xC2B2AE3Du)) | 1u
                             : 0u;
@@ -4159,160 +4150,13 @@ __global__ __launch_bounds__(256) void k_tiny_copy_rows(CopyArgs a) {
 
 
 
-// Segmented inclusive OR over teams of W lanes (W <= 32): a lane with `seen` set starts a segment
-// (team_seg_scan's shape, on the two halves of a 64-bit mask).
-template <int W>
-__device__ __forceinline__ unsigned long long team_seg_or(unsigned long long m, bool seen, int tl) {
-    int hi = (int)(m >> 32), lo = (int)(unsigned)m;
-#pragma unroll
-    for (int d = 1; d < (W < 16 ? W : 16); d <<= 1) {
-        const int oh = row_shr(hi, d), ol = row_shr(lo, d);
-        const int of = row_shr((int)seen, d);
-        const bool add = tl >= d && !seen;
-        hi |= add ? oh : 0;
-        lo |= add ? ol : 0;
-        seen = add ? of != 0 : seen;
-    }
-    if (W == 32) {  // rows 1, 3 take lane 15 / 47 of the row below (computed by every lane)
-        const int bh = row_bcast15<0xA>(hi), bl = row_bcast15<0xA>(lo);
-        const bool take = ((lane_id() >> 4) & 1) != 0 && !seen;
-        hi |= take ? bh : 0;
-        lo |= take ? bl : 0;
-    }
-    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-}
-
-// The symbolic tile-sort class (SYM_TILE, mhs_internal.hpp): a team of W lanes per row, K tile
-// products a lane (product p = i*W + lane in slot i: B row j's tile at st_j + p - excl_j, the A
-// entry j found by a binary search over the team's scan of the B rows' tile counts), sorted by
-// (tile, element) in registers with the masks parked in LDS by element; equal tiles are adjacent:
-// heads count the row's tiles, a segmented OR gives each tile's mask at its run's end, which writes
-// the (mask, key) pair at the tile's rank in the row-cache list.  nnz = sum of the ORs' popcounts.
-template <int W, int K>
-__device__ __forceinline__ void tile_rows(const SymArgs& a, int bid, int nb) {
-    static_assert(W * K == (1 << TILE_EB) && W <= 32 && (W & (W - 1)) == 0, "team shape");
-    const int count = a.stats->sym_count[SYM_TILE];
-    const int* list = a.list + (long long)(SYM_TILE - 1) * a.M;
-    const RowWalk rw(count, 256 / W, (int)(threadIdx.x / W), bid, nb);
-    extern __shared__ __attribute__((aligned(16))) char tile_smem[];
-    unsigned long long* ms = (unsigned long long*)tile_smem + (size_t)(threadIdx.x / W) * (W * K);
-    for (int it = rw.first; __ballot(it < rw.end) != 0; it += rw.stride) {
-        int lane = lane_id();
-        asm volatile("" : "+v"(lane));  // (team masks rebuilt per row: see tiny_rows)
-        const int tl = lane & (W - 1), tb = lane & ~(W - 1);
-        const unsigned long long tmask = ((1ull << W) - 1) << tb;
-        const unsigned long long below = tmask & (lane == 0 ? 0ull : (~0ull >> (64 - lane)));
-        const bool live = it < rw.end;
-        const int row = live ? list[it] : 0;
-        const int a0 = live ? a.Aptr[row] : 0;
-        const int nA = live ? a.Aptr[row + 1] - a0 : 0;
-        const int lo = live ? a.rlo[row] : 0;
-        const int R = live ? (int)a.grp[row] : 0;  // a group head: its rows share the count
-        int st = 0, len = 0;
-        if (tl < nA) {
-            const int4 m = a.bmeta[a.Acol[a0 + tl]];
-            st = m.x;
-            len = meta_ntiles(m);
-        }
-        const int incl = team_incl_scan<W>(len, tl);
-        const int tf = __shfl(incl, tb + W - 1);
-        const int excl = incl - len;
-        unsigned key[K];
-        int q[K];
-        bool valid[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const int p = i * W + tl;
-            int j = 0;
-#pragma unroll
-            for (int step = W / 2; step >= 1; step >>= 1) {
-                const int x = __shfl(incl, tb + j + step - 1);
-                j += x <= p ? step : 0;
-            }
-            valid[i] = p < tf;
-            const int src = tb + (valid[i] ? j : 0);
-            const int stj = __shfl(st, src);
-            const int exj = __shfl(excl, src);
-            q[i] = valid[i] ? stj + (p - exj) : 0;
-        }
-        int tcol[K];
-        unsigned long long mk[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            tcol[i] = a.btcol[q[i]];
-            mk[i] = a.btmask[q[i]];
-        }
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            key[i] = valid[i] ? ((unsigned)(tcol[i] - lo) << TILE_EB) | (unsigned)(i * W + tl) : 0xFFFFFFFFu;
-            ms[i * W + tl] = mk[i];
-        }
-        reg_bitonic<W, K>(key, tl);
-        wave_sync();
-        int tt[K];
-        unsigned long long mm[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const bool v = key[i] != 0xFFFFFFFFu;
-            tt[i] = v ? (int)(key[i] >> TILE_EB) : INT_MAX;
-            mm[i] = v ? ms[key[i] & (W * K - 1)] : 0ull;
-        }
-        wave_sync();  // the slice is rewritten by the team's next row
-        unsigned long long carry = 0ull;  // the open run's OR at the end of slot i-1
-        int rank0 = 0;                     // tiles in slots < i
-        int prev_last = -1;
-        long long nnz = 0;
-        unsigned long long* slot0 = (live && a.mcache) ? a.mcache + (size_t)row * a.mc_stride : nullptr;
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const int up = __shfl_up(tt[i], 1, W);
-            const int pc = tl == 0 ? (i == 0 ? -1 : prev_last) : up;
-            const bool head = tt[i] != INT_MAX && pc != tt[i];
-            const unsigned long long hb = __ballot(head) & tmask;
-            const bool seen = (hb & (below | (1ull << lane))) != 0;
-            unsigned long long orv = team_seg_or<W>(mm[i], head, tl);
-            orv |= seen ? 0ull : carry;
-            const int nc = __shfl_down(tt[i], 1, W);
-            const int nxt = i + 1 < K ? __shfl(tt[i + 1 < K ? i + 1 : i], tb) : INT_MAX;
-            const int next = tl == W - 1 ? nxt : nc;
-            const bool last = tt[i] != INT_MAX && next != tt[i];
-            if (live && last) {
-                nnz += __popcll(orv);
-                if (slot0) {
-                    const int pos = rank0 + __popcll(hb & (below | (1ull << lane))) - 1;
-                    for (int g = 0; g < R; ++g) {
-                        unsigned long long* sl = slot0 + (size_t)g * a.mc_stride;
-                        st_cache(&sl[pos], orv);
-                        st_cache(&reinterpret_cast<int*>(sl + a.mc_list)[pos], lo + tt[i]);
-                    }
-                }
-            }
-            carry = ((unsigned long long)(unsigned)__shfl((int)(orv >> 32), tb + W - 1) << 32) |
-                    (unsigned)__shfl((int)(unsigned)orv, tb + W - 1);
-            rank0 += __popcll(hb);
-            prev_last = __shfl(tt[i], tb + W - 1);
-        }
-#pragma unroll
-        for (int d = W / 2; d >= 1; d >>= 1) nnz += __shfl_xor(nnz, d);  // (xor stays inside the team)
-        if (live && tl < R) {
-            a.Cptr[row + tl] = (int)nnz;
-            a.ctiles[row + tl] = rank0;
-        }
-    }
-}
-constexpr int TILE_SYM_BLOCKS = 2048;  // persistent blocks of the tile-sort role in k_sym_common
-
 // The common symbolic bins in one launch (their sizes are on the device; an empty role
 // costs its blocks one load): blocks [0, wave_blocks) run the small-table wave bin,
-// the next every tiny class, blocks from tile_blk0 the tile-sort class -- fewer launches,
-// and the roles overlap.
+// the rest every tiny class -- one launch less, and the two overlap.
 template <int BYTES>
-__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_common(SymArgs a, TinyArgs t, int wave_blocks,
-                                                                              int tile_blk0) {
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_SYM) void k_sym_common(SymArgs a, TinyArgs t, int wave_blocks) {
     if ((int)blockIdx.x < wave_blocks)
         sym_wave_rows<BYTES>(a, (int)blockIdx.x, wave_blocks);
-    else if ((int)blockIdx.x >= tile_blk0)
-        tile_rows<TILE_W, TILE_K>(a, (int)blockIdx.x - tile_blk0, (int)gridDim.x - tile_blk0);
     else
         tiny_sym_rows(t, (int)blockIdx.x - wave_blocks);
 }
@@ -4395,8 +4239,8 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG, UU) hipLaunchKernelGGL((k_analyze<GG, UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, (w.tiny_num && MHS_SYM_SORT64 ? 1 : 0) | (w.tile_max << 8))
-#define MHS_ANALYZE_LANE(UU) hipLaunchKernelGGL((k_analyze_lane<UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, (w.tiny_num && MHS_SYM_SORT64 ? 1 : 0) | (w.tile_max << 8))
+#define MHS_ANALYZE(GG, UU) hipLaunchKernelGGL((k_analyze<GG, UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, w.tiny_num && MHS_SYM_SORT64)
+#define MHS_ANALYZE_LANE(UU) hipLaunchKernelGGL((k_analyze_lane<UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, w.tiny_num && MHS_SYM_SORT64)
     switch (G) {
     case 1:
         if (A.nnz < 4LL * A.M) MHS_ANALYZE_LANE(4);
@@ -4586,10 +4430,8 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
         t.blk0[TINY_SYMX_NC] = t.blk0[TINY_SYM_NC] + (MHS_SYM_SORT64 ? TINY_SYM_GRID : 0);  // class 4: a walk
         tiny_blocks = t.blk0[TINY_SYMX_NC];
     }
-    static_assert(256 / TILE_W * TILE_SORT_MAX * 8 <= WPB * SYM_WAVE_BYTES, "the tile role's mask stage fits the LDS");
-    const int tile_blocks = w.tile_max > 0 ? TILE_SYM_BLOCKS : 0;
-    hipLaunchKernelGGL(k_sym_common<SYM_WAVE_BYTES>, dim3(wave_blocks + tiny_blocks + tile_blocks), dim3(256),
-                       WPB * SYM_WAVE_BYTES, s, a, t, wave_blocks, wave_blocks + tiny_blocks);
+    hipLaunchKernelGGL(k_sym_common<SYM_WAVE_BYTES>, dim3(wave_blocks + tiny_blocks), dim3(256),
+                       WPB * SYM_WAVE_BYTES, s, a, t, wave_blocks);
 }
 
 // The rare bins (10 KiB waves, 32 KiB and 157 KiB block tables, global memory): one

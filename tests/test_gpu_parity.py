@@ -967,25 +967,3 @@ def test_nft_slots_skipped_under_memory_budget(tool):
         A.d_release_csr()
     finally:
         t2.close()
-
-
-@pytest.mark.parametrize("name", ["cage15-small", "webbase-1M", "cop20k_A", "scircuit"])
-def test_symbolic_tile_sort_class(tool, name, monkeypatch):
-    """Round 6: short rows over scattered tiles count by a register sort of their (tile, mask)
-    products (symbolic bin 12, two rows a wave) and leave a key-sorted row-cache list -- the
-    oracle's C with the class on (it must have run) and off (MHS_NO_TILE_SORT=1)."""
-    if name == "cage15-small":  # the cage15-like generator at 400 K rows
-        A = synth.sym_banded(400_000, 10.25, 48, 0.058, disp=3.5, seed=7)
-    else:
-        A = synth.SYNTH[name]()
-    t = check(tool, A, A)
-    if name in ("cage15-small", "webbase-1M"):
-        assert t.sym_bins[12] > 0, t.sym_bins
-    monkeypatch.setenv("MHS_NO_TILE_SORT", "1")
-    t2 = mhspgemm.Tool(tool.device)
-    try:
-        t = check(t2, A, A)
-        assert t.sym_bins[12] == 0, t.sym_bins
-    finally:
-        t2.close()
-        A.d_release_csr()
