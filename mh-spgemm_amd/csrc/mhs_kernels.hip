@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <functional>
 #include <type_traits>
 #include <vector>
@@ -4399,7 +4400,9 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
     if (M <= 0) return;
     SymArgs a = sym_args(A, w, M, N, Cptr);
     a.bin = SYM_WAVE;
-    const int wave_blocks = round8((M + WPB - 1) / WPB, MHS_SYM_WAVE_GRID);
+    static const int ab_cap = getenv("MHS_AB_SYMGRID") ? atoi(getenv("MHS_AB_SYMGRID")) : 0;  // (A/B, temporary)
+    static const int ab_m = getenv("MHS_AB_SYMGRID_M") ? atoi(getenv("MHS_AB_SYMGRID_M")) : (1 << 30);
+    const int wave_blocks = round8((M + WPB - 1) / WPB, (ab_cap > 0 && M >= ab_m) ? ab_cap : MHS_SYM_WAVE_GRID);
     TinyArgs t{};
     t.M = M;
     t.Aptr = A.ptr;

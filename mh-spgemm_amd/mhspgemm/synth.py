@@ -429,6 +429,8 @@ SYNTH = {
     "cop20k_A": cop20k_like,
     "cage15": cage15_like,
     "cage15-r5": cage15_banded,
+    # cage15-like without its long-range entries (the near band's share of the traffic)
+    "cage15-near": lambda: sym_banded(5_154_859, 10.25, 48, 0.0, disp=3.5, seed=7),
     # headline robustness variants
     "cant-s1": cant_s1,
     "cant-perturbed": cant_perturbed,
