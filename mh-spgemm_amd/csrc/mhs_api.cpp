@@ -839,6 +839,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         }
         const unsigned long long n = ctx->pub->stats.an_slots;
         other = ctx->pub->stats.an_other;
+        w.sym_big = other >= (1ull << 21);
         // slots pay where the tiny rows are (nearly) the whole product: elsewhere numeric's
         // tiny classes run beside the long rows' kernels anyway (measured: wb-edu-like +10%
         // with slots, 19% of its rows past the tiny classes; GAP-road- / delaunay-like -12% / -17%)

@@ -429,6 +429,7 @@ struct Work {
     void* gscratch;    // global-bin scratch
     size_t gscratch_bytes;
     const int* go;     // speculated numeric launches: run only when *go == 1 (k_scan's verdict); nullptr: always
+    int sym_big;       // the numeric-first probe counted >= 2^21 rows past the tiny classes: big symbolic wave grid
 };
 
 void launch_mask_b(const Csr& B, const Work& w, hipStream_t s);

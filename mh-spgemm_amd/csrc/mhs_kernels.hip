@@ -54,6 +54,7 @@ constexpr int MHS_COPY_CAP_BIG = 65536;  // the slot copy's block cap from 4 M r
 constexpr int MHS_NFT_GRID = 4096, MHS_NFT_GRID_BIG = 16384, MHS_NFT_BIG_M = 1 << 22;
 constexpr int MHS_TINY_PF = 1;  // tiny teams load their next row a round ahead (GAP-road-like -3 %, mac_econ-, scircuit-like -1 %)
 constexpr int MHS_SYM_WAVE_GRID = 2048;  // block cap of k_sym_common's wave rows (65536: cage15-like -3 %, cop20k-, webbase-, mac_econ-like +5 %)
+constexpr int MHS_SYM_WAVE_GRID_BIG = 65536;  // ... when the probe counted >= 2^21 table rows (Work::sym_big)
 constexpr int MHS_NUM_WSH_BIG = (1 << 21);  // small hash bins of at least this many rows: block cap MHS_NUM_WSH_BIG_GRID
 constexpr int MHS_NUM_WSH_BIG_GRID = 65536;  // (cage15-like -2.5 % over 16384; 65536 for every bin: offshore-, webbase-like +1.5 %)
 constexpr int MHS_NUM_WSX_GRID = 16384;  // ... of the small-row hash / direct launches (8192: cage15-like numeric +4.5 %, 4096: +13 %,
@@ -4400,9 +4401,9 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
     if (M <= 0) return;
     SymArgs a = sym_args(A, w, M, N, Cptr);
     a.bin = SYM_WAVE;
-    static const int ab_cap = getenv("MHS_AB_SYMGRID") ? atoi(getenv("MHS_AB_SYMGRID")) : 0;  // (A/B, temporary)
-    static const int ab_m = getenv("MHS_AB_SYMGRID_M") ? atoi(getenv("MHS_AB_SYMGRID_M")) : (1 << 30);
-    const int wave_blocks = round8((M + WPB - 1) / WPB, (ab_cap > 0 && M >= ab_m) ? ab_cap : MHS_SYM_WAVE_GRID);
+    // (the probe counted >= 2^21 rows past the tiny classes -- table rows, nearly all in this bin: the
+    // numeric hash bin's big-grid rule; r06i: cage15-like -3.2 %; wb-edu-like, 1.9 M such rows, keeps 2048)
+    const int wave_blocks = round8((M + WPB - 1) / WPB, w.sym_big ? MHS_SYM_WAVE_GRID_BIG : MHS_SYM_WAVE_GRID);
     TinyArgs t{};
     t.M = M;
     t.Aptr = A.ptr;
