@@ -81,6 +81,7 @@ struct mhs_ctx {
     hipStream_t aux[NAUX] = {};
     hipEvent_t fork_ev = nullptr, join_ev[NAUX] = {};
     hipEvent_t split_ev = nullptr;  // k_split_bins done (the split block launches wait for it)
+    bool split_on = false;          // a speculated plan's phase A split its block bins (phase B's launches)
     // launch plan speculation (SpecArgs, mhs_internal.hpp): the last hand-off's Stats and the
     // operands they belong to; MHS_NO_SPEC=1 turns it off
     struct PlanKey {
@@ -95,8 +96,7 @@ struct mhs_ctx {
     Stats plan_h{};
     long long gen = 0;        // bumped by every mhs_ctx_set_option (options change the pipeline)
     int* d_go = nullptr;      // k_scan's verdict on a speculated plan (device int)
-    int spec_nss = 1;         // streams of a speculated numeric phase (MHS_SPEC_NSS): the aux streams'
-                              // waits on a fork event that has not completed yet cost more than the overlap
+    int spec_nss = mhs_ctx::NAUX + 1;  // streams of a speculated numeric phase (MHS_SPEC_NSS: a cap, A/B)
 };
 
 namespace {
@@ -397,20 +397,27 @@ int numeric_streams(const mhs_ctx* ctx, const Stats& h) {
 
 // The numeric launches for `h` (grids, LDS) on the call's stream, the heavy bins dealt over
 // the aux streams, which join the call's stream again.
+// Phases of a numeric launch sequence: ALL (after the hand-off: every launch), and the two halves
+// of a speculated plan -- SPEC_A, queued right behind k_scan before its Stats are known: the fork
+// event, the block-bin split and the launches dealt to the call's stream; SPEC_B, after the host
+// has seen k_scan's verdict: the aux streams' launches (their wait on the fork event then finds
+// it complete -- waits on a pending one measured slower than the whole hand-off, r06b) and joins.
+enum NumPhase { NUM_ALL = 0, NUM_SPEC_A = 1, NUM_SPEC_B = 2 };
+
 int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const Stats& h, const mhs_csr& out,
-                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int phase = NUM_ALL) {
     hipStream_t s = ctx->stream;
     // several heavy bins: deal them over the aux streams (fork/join costs ~10-20 us,
     // so only when there are at least 3 launches of a product worth it)
     hipStream_t ss[mhs_ctx::NAUX + 1] = {s};
     int nss = numeric_streams(ctx, h);
-    if (w.go) nss = std::min(nss, ctx->spec_nss);  // speculated: the fork event is still pending (see spec_nss)
+    if (w.go) nss = std::min(nss, ctx->spec_nss);  // (MHS_SPEC_NSS: a speculated plan on fewer streams)
+    for (int i = 1; i < nss; ++i) ss[i] = ctx->aux[i - 1];
     hipError_t fe = hipSuccess;
-    if (nss > 1 && ev0) MHS_HIP(hipEventRecord(ev0, s));  // (several streams: events of their own)
-    if (nss > 1) {
-        MHS_HIP(hipEventRecord(ctx->fork_ev, s));
-        for (int i = 1; i < nss; ++i) ss[i] = ctx->aux[i - 1];
-    }
+    const bool first = phase != NUM_SPEC_B, last = phase != NUM_SPEC_A;
+    if (phase == NUM_SPEC_B && nss == 1) return MHS_OK;  // (phase A launched everything)
+    if (first && nss > 1 && ev0) MHS_HIP(hipEventRecord(ev0, s));  // (several streams: events of their own)
+    if (first && nss > 1) MHS_HIP(hipEventRecord(ctx->fork_ev, s));
     // the aux streams wait for the fork (everything before numeric) -- set up after the first
     // numeric launch has gone out on the call's stream (launch_numeric)
     auto fork = [&]() {
@@ -423,18 +430,29 @@ int run_numeric(mhs_ctx* ctx, const Csr& a, const Csr& b, const Work& w, const S
     // the other bins start at once (wb-edu-like: 0.33 ms off the numeric phase's start)
     // (and only from 2^MHS_SPLIT_FLOP_LOG2 products: on scircuit-like the partition and its event
     // wait cost more than the split saves -- numeric 0.146 -> 0.119 ms unsplit)
-    const bool split = nss > 1 && ctx->split && h.flop >= (1ull << MHS_SPLIT_FLOP_LOG2) &&
-                       launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);
-    if (split) MHS_HIP(hipEventRecord(ctx->split_ev, s));
-    ctx->stat[MHS_STAT_SPLIT] += split;
-    ctx->stat[MHS_STAT_MULTI_STREAM] += nss > 1;
+    const bool want_split = nss > 1 && ctx->split && h.flop >= (1ull << MHS_SPLIT_FLOP_LOG2);
+    bool split = false;
+    if (first) {
+        split = want_split && launch_split_bins(w, h, a.M, out.ptr, s, ctx->dense_span_max);
+        if (split) MHS_HIP(hipEventRecord(ctx->split_ev, s));
+        ctx->split_on = split;
+        ctx->stat[MHS_STAT_SPLIT] += split;
+        ctx->stat[MHS_STAT_MULTI_STREAM] += nss > 1;
+    } else {
+        split = ctx->split_on;  // (phase A's decision)
+    }
+    const int only = phase == NUM_SPEC_A ? 1 : phase == NUM_SPEC_B ? ~1 : ~0;
     const int used = launch_numeric(a, b, w, h, out.ptr, out.col, out.val, ss, nss, NUM_GLOBAL_GRID,
                                     ctx->dense_span_max, split, split ? ctx->split_ev : nullptr,
                                     nss > 1 ? std::function<bool()>(fork) : std::function<bool()>(),
-                                    nss == 1 ? ev0 : nullptr, nss == 1 ? ev1 : nullptr);
+                                    nss == 1 ? ev0 : nullptr, nss == 1 ? ev1 : nullptr, only);
     if (nss == 1 && (used & (1 << 30))) {  // (no launch carried them)
         if (ev0) MHS_HIP(hipEventRecord(ev0, s));
         if (ev1) MHS_HIP(hipEventRecord(ev1, s));
+    }
+    if (!last) {
+        MHS_HIP(hipGetLastError());
+        return MHS_OK;
     }
     // joins first: an error below must not leave aux-stream work behind the call's stream
     for (int i = 1; i < nss; ++i)
@@ -874,11 +892,9 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         key.mc_list = mc_list;
     }
     const bool plannable = ctx->spec && M > 0 && !probe && !fork_sym;
-    // (only plans whose numeric phase runs on one stream: dealt over the aux streams, the launches
-    // would wait on a fork event k_scan has not reached yet, and those waits measured slower than
-    // the hand-off they save -- scircuit-like +3..18 %, cop20k-like +7 %; r06b)
-    const bool spec = plannable && ctx->plan_valid && ctx->plan_key == key &&
-                      std::min(numeric_streams(ctx, ctx->plan_h), ctx->spec_nss) == numeric_streams(ctx, ctx->plan_h);
+    // (a plan dealt over several streams queues only its call-stream launches ahead of k_scan: see
+    // NumPhase)
+    const bool spec = plannable && ctx->plan_valid && ctx->plan_key == key;
     const Stats ph = ctx->plan_h;  // (a copy: this call replaces the plan)
     ctx->plan_valid = false;  // (set again by this call's success)
     // ---- Calculate_C_nnz ------------------------------------------------------------
@@ -941,7 +957,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
                 if (ph.nnzC > 0) {
                     out.nnz = (int)ph.nnzC;
                     rc = run_numeric(ctx, a, b, w, ph, out, nring ? ctx->nev[2 * slot] : nullptr,
-                                     nring ? ctx->nev[2 * slot + 1] : nullptr);
+                                     nring ? ctx->nev[2 * slot + 1] : nullptr, NUM_SPEC_A);
                     if (rc) {
                         (void)hipStreamSynchronize(s);
                         mhs_ctx_recycle(ctx, &out);
@@ -967,6 +983,16 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         }
         memcpy(&h, (const void*)&ctx->pub->stats, sizeof(Stats));
         ctx->stats_zero = true;  // k_scan's last block cleared them after publishing
+        if (launched && !h.err && stats_same_plan(h, ph) && ph.nnzC > 0) {
+            // the plan holds: its aux-stream launches and joins (phase B)
+            rc = run_numeric(ctx, a, b, w, ph, out, nring ? ctx->nev[2 * slot] : nullptr,
+                             nring ? ctx->nev[2 * slot + 1] : nullptr, NUM_SPEC_B);
+            if (rc) {
+                (void)hipStreamSynchronize(s);
+                mhs_ctx_recycle(ctx, &out);
+                return rc;
+            }
+        }
         if (launched && (h.err || !stats_same_plan(h, ph))) {
             // the plan was not this call's: its kernels returned at once (k_scan wrote go = 0);
             // every array is rewritten by a call without speculation

@@ -458,7 +458,7 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr,
                    int* Ccol, double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max,
                    bool split, hipEvent_t split_ev = nullptr, const std::function<bool()>& fork = nullptr,
-                   hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+                   hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr, int only = ~0);
 // numeric launches a call makes for these bin counts (the 32-lane tiny classes share one; a
 // split block bin makes two)
 int numeric_launches(const Stats& h);

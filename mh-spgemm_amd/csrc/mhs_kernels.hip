@@ -4622,7 +4622,8 @@ struct NumLaunch {
 
 int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, int* Cptr, int* Ccol,
                    double* Cval, const hipStream_t* ss, int nss, int global_grid, int dense_span_max, bool split,
-                   hipEvent_t split_ev, const std::function<bool()>& fork, hipEvent_t ev_start, hipEvent_t ev_stop) {
+                   hipEvent_t split_ev, const std::function<bool()>& fork, hipEvent_t ev_start, hipEvent_t ev_stop,
+                   int only) {
     std::vector<NumLaunch> L;
     auto add = [&](std::function<void(hipStream_t)> go) { L.push_back(NumLaunch{std::move(go)}); };
     NumArgs a{};
@@ -4854,12 +4855,22 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     // hand-off gap 46 -> ? us)
     // (a failed fork -- the aux streams' wait on the fork event -- sends every later launch to
     // ss[0]: no aux-stream launch may run without its dependency on the pre-numeric work)
+    // `only`: the streams (bit k: ss[k]) whose launches go out in this call -- a speculated plan
+    // deals the same list twice, the call stream's share first (see NumPhase in mhs_api.cpp)
     int used = 0;
     int n = nss < 1 ? 1 : (nss > 8 ? 8 : nss);
-    const bool evs = n == 1 && !L.empty() && (ev_start || ev_stop);  // (single stream only: see num_launch)
+    const bool evs = n == 1 && !L.empty() && (ev_start || ev_stop) && (only & 1);  // (single stream only: see num_launch)
+    bool forked = false;
     for (size_t i = 0; i < L.size(); ++i) {
-        if (i == 1 && n > 1 && fork && !fork()) n = 1;
-        const int k = n > 1 ? (int)(i % n) : 0;
+        int k = n > 1 ? (int)(i % n) : 0;
+        if (!((only >> k) & 1)) continue;
+        if (k != 0 && !forked) {  // the aux streams' waits, before their first launch
+            forked = true;
+            if (fork && !fork()) {
+                n = 1;  // (a failed fork: the rest on ss[0])
+                k = 0;
+            }
+        }
         used |= 1 << k;
         if (evs && i == 0) t_num_start = ev_start;
         if (evs && i + 1 == L.size()) t_num_stop = ev_stop;
@@ -4867,7 +4878,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
     }
     t_num_start = t_num_stop = nullptr;
     if (!evs && (ev_start || ev_stop)) used |= 1 << 30;  // the caller records the events itself
-    if (L.size() <= 1 && n > 1 && fork) (void)fork();  // (the caller's error check expects the fork)
+    if (!forked && n > 1 && fork && (only & ~1)) (void)fork();  // (the caller's error check expects the fork)
     return used;
 }
 }  // namespace mhs
