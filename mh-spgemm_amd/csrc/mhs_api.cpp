@@ -235,7 +235,7 @@ Layout plan(int M, int MB, long long nnzA, long long nnzB, int mc_list, int M_to
     static_assert((int)NUM_NB >= (int)SYM_NB, "bin_list holds either phase's bins");
     L.bin_list = take((size_t)(NUM_NB - 1) * M * 4);
     L.blkflop = take(((size_t)analyze_blocks(nnzA, M) + 1) * 8);
-    L.scan_part = take(nscan * 8 + (size_t)CURSOR_INTS * 4);  // look-back words, then the row cursors
+    L.scan_part = take(nscan * 8 + (size_t)ZERO_INTS * 4);  // look-back words, then the row cursors and bin counters
     L.mcache = take((size_t)M * mc_stride(mc_list) * 8);
     L.spill_cap = spill_cap(nnzB);
     if (M_total > M && M_total > 0)  // a row chunk: its share of the region (spill lists belong to rows)

@@ -36,6 +36,17 @@ constexpr int SCAN_ITEMS = MHS_SCAN_ITEMS;  // rows per block (of 1024 threads) 
 constexpr int CURSOR_SLOTS = 40;
 constexpr int CURSOR_STRIDE = 16;  // ints
 constexpr int CURSOR_INTS = CURSOR_SLOTS * 8 * CURSOR_STRIDE;
+// Bin-list counters (round 6): the per-(block, bin) atomics of k_bin_list / k_scan that reserve a
+// block's places in a bin's list, one 128-byte line per bin (they were the 16 ints of Stats'
+// sym_count / num_count, one line: every block's reservations serialised on it), then k_bin_list's
+// done counter.  After the cursors, zeroed with them by k_analyze; the last block of each kernel
+// copies its totals into Stats.
+#ifndef MHS_BINCNT_STRIDE
+#define MHS_BINCNT_STRIDE 32
+#endif
+constexpr int BINCNT_STRIDE = MHS_BINCNT_STRIDE;  // ints (128 bytes; 1: the counters on one line, A/B)
+constexpr int BINCNT_INTS = (2 * NBINS + 1) * BINCNT_STRIDE;
+constexpr int ZERO_INTS = CURSOR_INTS + BINCNT_INTS;  // look-back state + cursors + bin counters: zeroed per call
 constexpr int SPILL_PARTS = 64;        // spill-list bump counters: cursor slots 32..39
 constexpr int SPILL_CURSOR_SLOT = 32;
 constexpr int BLOCK_BIG_SLOT = 28;     // cursors of the block bins' hub-row launches (28: 256, 29: 1024 threads)
@@ -421,7 +432,7 @@ struct Work {
     unsigned long long* blkflop;  // per-block flop partials of k_analyze
     int nflop;                    // their count
     int* scan_part;    // k_scan's look-back state: one 64-bit word per block (flag | prefix)
-    int* cursors;      // CURSOR_INTS row cursors (after the look-back words)
+    int* cursors;      // CURSOR_INTS row cursors (after the look-back words), then BINCNT_INTS bin counters
     unsigned long long* mcache;   // [M][mc_stride] tile masks / tile lists (symbolic -> numeric)
     int mc_list;                  // list cap (see mlisted)
     SpillArea spill;              // tile lists of rows past mc_list (symbolic -> numeric)

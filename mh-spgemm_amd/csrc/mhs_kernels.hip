@@ -2693,8 +2693,9 @@ __global__ __launch_bounds__(1024) void k_sym_rare(SymArgs a, NearArgs np) {
 
 // Append a 1024-thread block's SCAN_ITEMS rows (blockIdx*SCAN_ITEMS + j, bins in
 // binof[j]) to contiguous per-bin lists: bin x's rows at list + (x-1)*M, cursor
-// cnt[x].  The block's rows keep row order; one atomic per (block, bin) reserves
-// their places (the grids that call this have M/4096 blocks: little contention).
+// cnt[x * BINCNT_STRIDE] (a 128-byte line per bin: on one line the blocks' reservations
+// serialised -- round 6).  The block's rows keep row order; one atomic per (block, bin)
+// reserves their places.
 template <int NB, int PER>
 __device__ void append_block_rows(const unsigned char* binof, long long M, int* __restrict__ cnt,
                                   int* __restrict__ list, int blk) {
@@ -2719,7 +2720,7 @@ __device__ void append_block_rows(const unsigned char* binof, long long M, int* 
         const int c = lane < PER * 16 ? wc[w][lane] : 0;
         const int inc = wave_incl_scan(c);
         if (lane < PER * 16) wc[w][lane] = inc - c;
-        if (lane == 63) nbase[w] = inc ? atomicAdd(&cnt[w], inc) : 0;
+        if (lane == 63) nbase[w] = inc ? atomicAdd(&cnt[w * BINCNT_STRIDE], inc) : 0;
     }
     __syncthreads();
 #pragma unroll
@@ -2767,7 +2768,7 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
                                                    const unsigned char* __restrict__ asame,
                                                    unsigned char* __restrict__ grp, int groups,
                                                    int* __restrict__ list, const unsigned char* __restrict__ nft_bin,
-                                                   Stats* __restrict__ stats, NearCand nc) {
+                                                   Stats* __restrict__ stats, NearCand nc, int* __restrict__ bincnt) {
     __shared__ unsigned char binof[1024 * PER];
     // links of rows [blk0 - RG_BREAK, blk0 + ITEMS + RG_MAX): a row's group reads its run back
     // to the last RG_BREAK boundary and its group forward
@@ -2838,7 +2839,11 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
     if (threadIdx.x == 0 && ncand_s) nbase_s = atomicAdd(&stats->near_heads, ncand_s);
     __syncthreads();
     for (int q = 0; q < cand_n; ++q) nc.list[nbase_s + at + q] = cand_e[q];
-    append_block_rows<SYM_NB, PER>(binof, M, stats->sym_count, list, (int)blockIdx.x);
+    append_block_rows<SYM_NB, PER>(binof, M, bincnt, list, (int)blockIdx.x);
+    // the last block leaves the totals in Stats (the symbolic launches read them there)
+    if (last_block_done(bincnt + 2 * NBINS * BINCNT_STRIDE) && threadIdx.x < NBINS)
+        stats->sym_count[threadIdx.x] = __hip_atomic_load(bincnt + threadIdx.x * BINCNT_STRIDE, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ int num_bin_of(int n, int flop, int span, int t, int* gneed,
@@ -2908,7 +2913,8 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
                                                const unsigned long long* __restrict__ blkflop, int nflop, int nft,
                                                long long* __restrict__ tslot, const int* __restrict__ gna,
                                                int4* __restrict__ bmeta_near,
-                                               const unsigned char* __restrict__ sym_bin, SpecArgs spec) {
+                                               const unsigned char* __restrict__ sym_bin, SpecArgs spec,
+                                               int* __restrict__ bincnt) {
     constexpr int ITEMS = 1024 * PER;  // PER consecutive rows per thread
     static_assert(PER == 1 || PER == 4, "launch_scan_classify instantiates these");
     __shared__ long long ws[16];
@@ -3123,8 +3129,12 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         off += v[k];
     }
     __syncthreads();
-    append_block_rows<NUM_NB, PER>(nbin_of, M, stats->num_count, list, bid);
+    append_block_rows<NUM_NB, PER>(nbin_of, M, bincnt, list, bid);
     if (!last_block_done(&stats->final_done)) return;
+    if (threadIdx.x < NBINS)  // the bins' totals (bin-list counters) into Stats
+        stats->num_count[threadIdx.x] =
+            __hip_atomic_load(bincnt + threadIdx.x * BINCNT_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
     if (pub) {
         if (nonfin && threadIdx.x == 0) stats->near_verified = 0;  // (no union runs: nothing to copy)
         __syncthreads();
@@ -4241,8 +4251,8 @@ void launch_analyze(const Csr& A, const Work& w, int MB, hipStream_t s, int* Cpt
     int G, blocks;
     analyze_geometry(A.nnz, A.M, &G, &blocks);
     const dim3 grid(blocks), blk(256);
-#define MHS_ANALYZE(GG, UU) hipLaunchKernelGGL((k_analyze<GG, UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, w.tiny_num && MHS_SYM_SORT64)
-#define MHS_ANALYZE_LANE(UU) hipLaunchKernelGGL((k_analyze_lane<UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + CURSOR_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, w.tiny_num && MHS_SYM_SORT64)
+#define MHS_ANALYZE(GG, UU) hipLaunchKernelGGL((k_analyze<GG, UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + ZERO_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, w.tiny_num && MHS_SYM_SORT64)
+#define MHS_ANALYZE_LANE(UU) hipLaunchKernelGGL((k_analyze_lane<UU>), grid, blk, 0, s, A.M, MB, A.ptr, A.col, w.bmeta, w.bhi, w.rflop, w.rtflop, w.rlo, w.rhi, w.ctiles, w.sym_bin, Cptr, w.blkflop, w.asame, w.stats, (unsigned long long*)w.scan_part, (A.M + 1 + SCAN_ITEMS - 1) / SCAN_ITEMS + 1 + ZERO_INTS / 2, w.nft_bin, (w.near_list && !w.nft_bin) ? w.nsig : nullptr, w.tiny_num && MHS_SYM_SORT64)
     switch (G) {
     case 1:
         if (A.nnz < 4LL * A.M) MHS_ANALYZE_LANE(4);
@@ -4274,10 +4284,10 @@ void launch_bin_list(const Csr& A, const Work& w, hipStream_t s) {
     const NearCand nc{w.nsig, (w.groups && !nb) ? w.near_list : nullptr};
     if (scan_per(A.M) == 4)
         hipLaunchKernelGGL(k_bin_list<4>, dim3((A.M + 4095) / 4096), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
-                           w.groups, w.bin_list, nb, w.stats, nc);
+                           w.groups, w.bin_list, nb, w.stats, nc, w.cursors + CURSOR_INTS);
     else
         hipLaunchKernelGGL(k_bin_list<1>, dim3((A.M + 1023) / 1024), dim3(1024), 0, s, A.M, w.sym_bin, w.asame, w.grp,
-                           w.groups, w.bin_list, nb, w.stats, nc);
+                           w.groups, w.bin_list, nb, w.stats, nc, w.cursors + CURSOR_INTS);
 }
 
 static NearArgs near_args(const Csr& A, const Work& w, const int* Cptr);  // (with the symbolic launchers)
@@ -4493,7 +4503,8 @@ void launch_scan_classify(int M, const Work& w, int* Cptr, const int* Aptr, hipS
 #define MHS_SCAN(P)                                                                                                \
     hipLaunchKernelGGL(k_scan<P>, dim3(nb), dim3(1024), 0, s, M, Cptr, (unsigned long long*)w.scan_part, w.rflop,  \
                        w.rlo, w.rhi, w.ctiles, w.grp, Aptr, w.bin_list, w.stats, dense_span_max, pub, seq, w.tiny_num, \
-                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, w.gna, w.near_b ? w.bmeta : nullptr, w.sym_bin, spec)
+                       w.blkflop, w.nflop, w.sc_col != nullptr, w.tslot, w.gna, w.near_b ? w.bmeta : nullptr, w.sym_bin, spec, \
+                       w.cursors + CURSOR_INTS + NBINS * BINCNT_STRIDE)
     if (per == 4) MHS_SCAN(4);
     else MHS_SCAN(1);
 #undef MHS_SCAN
