@@ -46,7 +46,7 @@ constexpr int CURSOR_INTS = CURSOR_SLOTS * 8 * CURSOR_STRIDE;
 #endif
 constexpr int BINCNT_STRIDE = MHS_BINCNT_STRIDE;  // ints (128 bytes; 1: the counters on one line, A/B)
 constexpr int BINCNT_INTS = (2 * NBINS + 1) * BINCNT_STRIDE;
-constexpr int ZERO_INTS = CURSOR_INTS + BINCNT_INTS;  // look-back state + cursors + bin counters: zeroed per call
+constexpr int ZERO_INTS = (CURSOR_INTS + BINCNT_INTS + 1) & ~1;  // cursors + bin counters, zeroed per call in 8-byte words
 constexpr int SPILL_PARTS = 64;        // spill-list bump counters: cursor slots 32..39
 constexpr int SPILL_CURSOR_SLOT = 32;
 constexpr int BLOCK_BIG_SLOT = 28;     // cursors of the block bins' hub-row launches (28: 256, 29: 1024 threads)
