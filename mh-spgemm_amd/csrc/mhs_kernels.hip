@@ -183,6 +183,26 @@ extern "C" int mhs_diag_guard(unsigned long long* out) {
 #define MHS_GUARD(H, where, key)
 #endif
 
+// k_scan / k_bin_list phase stamps (diagnostic builds, -DMHS_SCAN_STAMPS=1; tools/diag/scan_stamps.py):
+// thread 0 of every block writes s_memtime at each phase boundary -- [block][16]: k_scan 0..7,
+// k_bin_list 8..11
+#ifndef MHS_SCAN_STAMPS
+#define MHS_SCAN_STAMPS 0
+#endif
+#if MHS_SCAN_STAMPS
+__device__ unsigned long long* g_scandiag;
+extern "C" int mhs_diag_setup_scan(int nblocks, unsigned long long** dev) {
+    hipError_t e = hipMalloc((void**)dev, (size_t)nblocks * 128);
+    if (e == hipSuccess) e = hipMemset(*dev, 0, (size_t)nblocks * 128);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_scandiag), dev, sizeof(void*));
+    return (int)e;
+}
+#define MHS_SCSTAMP(b, k) \
+    do { if (threadIdx.x == 0 && g_scandiag) g_scandiag[(size_t)(b) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define MHS_SCSTAMP(b, k)
+#endif
+
 namespace mhs {
 
 // ------------------------------------------------------------------ helpers ---
@@ -2775,6 +2795,7 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
     constexpr int LK = 1024 * PER + RG_BREAK + RG_MAX;
     __shared__ unsigned char lk_s[LK];
     __shared__ int ncand_s, nbase_s;  // the block's near candidates: one counter add per block
+    MHS_SCSTAMP(blockIdx.x, 8);
     if (threadIdx.x == 0) ncand_s = 0;
     const long long lbase = (long long)blockIdx.x * (1024 * PER) - RG_BREAK;
     // link of row r to row r-1: 1 = the same A pattern, 2 = a near candidate (see GRP_NEAR;
@@ -2839,7 +2860,9 @@ __global__ __launch_bounds__(1024) void k_bin_list(int M, const unsigned char* _
     if (threadIdx.x == 0 && ncand_s) nbase_s = atomicAdd(&stats->near_heads, ncand_s);
     __syncthreads();
     for (int q = 0; q < cand_n; ++q) nc.list[nbase_s + at + q] = cand_e[q];
+    MHS_SCSTAMP(blockIdx.x, 9);  // (classified)
     append_block_rows<SYM_NB, PER>(binof, M, bincnt, list, (int)blockIdx.x);
+    MHS_SCSTAMP(blockIdx.x, 10);  // (appended)
     // the last block leaves the totals in Stats (the symbolic launches read them there)
     if (last_block_done(bincnt + 2 * NBINS * BINCNT_STRIDE) && threadIdx.x < NBINS)
         stats->sym_count[threadIdx.x] = __hip_atomic_load(bincnt + threadIdx.x * BINCNT_STRIDE, __ATOMIC_RELAXED,
@@ -2936,6 +2959,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         bid = bid_s;
     }
     const int base = bid * ITEMS + threadIdx.x * PER;
+    MHS_SCSTAMP(bid, 0);
     // every load of the block's rows issues here, ahead of the first barrier (the classification
     // below needs none of the prefix): one round trip for the counts and the row scalars
     unsigned long long fpart = 0;  // the block's share of k_analyze's per-block product partials
@@ -2979,6 +3003,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         woff += k < w ? ws[k] : 0;
         total += ws[k];
     }
+    MHS_SCSTAMP(bid, 1);  // (counts loaded, block scan done)
     // the block's aggregate goes out first: successors' look-backs need it
     if (threadIdx.x == 0 && bid > 0)
         __hip_atomic_store(&state[bid], LB_AGG | (unsigned long long)total, __ATOMIC_RELAXED,
@@ -3074,6 +3099,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         }
     }
     __syncthreads();
+    MHS_SCSTAMP(bid, 2);  // (classified)
     if (threadIdx.x < 8 && agg_s[threadIdx.x]) {
         const int k = threadIdx.x, v = agg_s[k];
         if (k < 2) atomicMax(&stats->num_wave_need[k], v);
@@ -3121,6 +3147,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         }
     }
     __syncthreads();
+    MHS_SCSTAMP(bid, 3);  // (look-back done)
     long long off = excl_s + woff + inc - loc;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -3129,8 +3156,11 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         off += v[k];
     }
     __syncthreads();
+    MHS_SCSTAMP(bid, 4);  // (row_ptr written)
     append_block_rows<NUM_NB, PER>(nbin_of, M, bincnt, list, bid);
+    MHS_SCSTAMP(bid, 5);  // (appended)
     if (!last_block_done(&stats->final_done)) return;
+    MHS_SCSTAMP(bid, 6);  // (the last block)
     if (threadIdx.x < NBINS)  // the bins' totals (bin-list counters) into Stats
         stats->num_count[threadIdx.x] =
             __hip_atomic_load(bincnt + threadIdx.x * BINCNT_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3142,6 +3172,7 @@ __global__ __launch_bounds__(1024) void k_scan(int M, int* __restrict__ Cptr,
         // call's Stats are the plan's (the host checks the same on the published copy)
         if (spec.go && threadIdx.x == 0) *spec.go = (stats->err == 0 && stats_same_plan(*stats, spec.expect)) ? 1 : 0;
         publish_stats(stats, pub, seq);
+        MHS_SCSTAMP(bid, 7);  // (published)
         // the host has its copy: leave the device Stats zeroed for the next call (nothing
         // after this kernel reads them), which saves that call a memset launch
         __syncthreads();
