@@ -27,7 +27,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--lib", default="")
+    ap.add_argument("--no-events", action="store_true", help="no numeric-phase hipEvents in the timed steps")
     args = ap.parse_args()
+    args.no_events |= os.environ.get("MHS_PIPE_NO_EVENTS", "0") != "0"  # (A/B variants are env strings)
     if args.lib:  # (read by mhspgemm._lib at import)
         os.environ["MHS_LIB"] = str(Path(args.lib) / "libmhspgemm.so")
     import numpy as np
@@ -49,7 +51,7 @@ def main():
         ms_l, nm_l = [], []
         for r in range(args.reps):
             tool.set_option(L.MHS_OPT_SYNC, 0)
-            tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, steps)
+            tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, 0 if args.no_events else steps)
             for _ in range(args.warmup):
                 C, _ = mhspgemm.spgemm(tool, A, A, timing=False)
                 C.release()
@@ -60,7 +62,7 @@ def main():
                 C.release()
             torch.cuda.synchronize()
             ms_l.append((time.perf_counter() - t0) / steps * 1e3)
-            nm_l.append(float(np.mean(tool.numeric_ms(steps))))
+            nm_l.append(0.0 if args.no_events else float(np.mean(tool.numeric_ms(steps))))
             tool.set_option(L.MHS_OPT_SYNC, 1)
             tool.set_option(L.MHS_OPT_NUMERIC_EVENTS, 0)
         ms = float(np.median(ms_l))
