@@ -1,4 +1,4 @@
-"""Variants of a stand-in for kernel attribution (tools/r05_diag3.sh): scircuit-like with and
+"""Variants of a stand-in for kernel attribution (a round-5 diagnostic run): scircuit-like with and
 without its 20 hub rows / hub columns.  usage: python tools/anatomy.py <variant> -> pipelined
 steps of that matrix (tools/pipe.py's loop), for a rocprofv3 kernel trace."""
 import sys

@@ -8,6 +8,9 @@
 #   tools/gpu.sh trace <tag> "<matrices>" ["ENV=.."]  kernel timelines of pipelined steps (rocprofv3)
 #   tools/gpu.sh prof <tag> <matrix> [passes]     rocprofv3 kernel stats + FETCH/WRITE passes of
 #                                                  bench.py --matrix <matrix> (tools/bench_profile.sh)
+#   tools/gpu.sh sweep <tag> ["<matrices>"]       synchronised calls with per-phase events, median of 5,
+#                                                  rocSPARSE beside them (tools/sweep.py), every stand-in
+#   tools/gpu.sh hbm <tag>                        the HBM peak shapes of mhs_hbm.hip (per-shape rates)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -o pipefail
 export TMPDIR=/tmp MHS_SYNTH_CACHE=/tmp/mhs_synth
@@ -43,7 +46,20 @@ trace)
 prof)
   bash tools/bench_profile.sh $tag "$3" "$4" > $out/prof.log 2>&1 || { tail -20 $out/prof.log; exit 1; }
   tail -8 $out/prof.log ;;
+sweep)
+  mats=${3:-"cant cant-s1 cant-perturbed webbase-1M mac_econ_fwd500 scircuit cop20k_A cage15 pdb1HYS pwtk cage12 hood rma10 shipsec1 offshore wb-edu GAP-road delaunay_n24"}
+  for m in $mats; do
+    timeout -k 10 300 python3 tools/sweep.py $m --reps 5 --vendor >> $out/sweep_all.jsonl 2>> $out/sweep.err \
+      || { echo "$m failed"; tail -5 $out/sweep.err; exit 1; }
+    echo "$m done"
+  done
+  python3 tools/baseline_table.py $out/sweep_all.jsonl ;;
+hbm)
+  MHS_HBM_VERBOSE=1 timeout -k 10 200 python3 -c "
+import sys; sys.path[:0]=['.','mh-spgemm_amd']
+import mhspgemm; t=mhspgemm.Tool(0); print(t.hbm_peak(2<<30, 10)); t.close()" > $out/hbm.log 2>&1 || { tail -5 $out/hbm.log; exit 1; }
+  grep -v amdgpu $out/hbm.log ;;
 *)
-  echo "usage: tools/gpu.sh check|ab|bench|prof <tag> ..."; exit 2 ;;
+  echo "usage: tools/gpu.sh check|ab|bench|trace|prof|sweep|hbm <tag> ..."; exit 2 ;;
 esac
 echo GPUDONE $mode $tag
