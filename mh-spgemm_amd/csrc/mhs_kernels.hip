@@ -3526,9 +3526,11 @@ __device__ __forceinline__ void num_row_body(const Team& tm, const NumArgs& a, i
         for (int g = 0; g < (GROUPED ? R : 1); ++g)
             store_vals(a.Cval + c0 + g * n, acc + g * stride, n, tm.rank(), Team::size);
         tm.sync();
+        MHS_BSTAMP(6);  // (stamps builds: the output phase split in three -- values, staging, columns)
         int* cb = (int*)acc;
         stage_cols<MODE != NM_HASH>(E, H, lo, cb, tm.rank(), Team::size);
         tm.sync();
+        MHS_BSTAMP(7);
         store_cols(a.Ccol + c0, cb, n, GROUPED ? R : 1, tm.rank(), Team::size);
     }
     tm.sync();

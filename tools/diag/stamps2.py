@@ -32,14 +32,17 @@ for i in range(3):
 buf = np.zeros(A.M * 8, np.uint64)
 assert L.mhs_memcpy(tool.ctx, ctypes.c_void_p(buf.ctypes.data), dev, buf.nbytes, 1) == 0
 ph = buf.reshape(A.M, 8).astype(np.float64)
-heads = ph[:, :6].sum(1) > 0
-names = ["prologue", "tiles(load/build)", "bases", "clear_acc", "accumulate", "output"]
+heads = ph[:, :8].sum(1) > 0
+names = ["prologue", "tiles(load/build)", "bases", "clear_acc", "accumulate", "output(cols)"]
 print("heads", heads.sum(), "of", A.M, flush=True)
+if ph[heads, 6:8].sum() > 0:  # table rows split their output: values [6], column staging [7], columns [5]
+    print(f"{'output: values':20s} {ph[heads, 6].mean():10.0f} cycles/head")
+    print(f"{'output: col staging':20s} {ph[heads, 7].mean():10.0f} cycles/head")
 for k, nm in enumerate(names):
     print(f"{nm:20s} {ph[heads, k].mean():10.0f} cycles/head")
-tot = ph[heads, :6].sum()
+tot = ph[heads, :8].sum()
 print("sum cycles over heads %.3e ; numeric ms %.4f" % (tot, t.Numeric))
-tot_r = ph[:, :6].sum(1)
+tot_r = ph[:, :8].sum(1)
 thr = np.percentile(tot_r[heads], 99)
 slow = heads & (tot_r >= thr)
 print("slowest 1%% rows: %d rows, mean total %.0f cycles" % (slow.sum(), tot_r[slow].mean()))
