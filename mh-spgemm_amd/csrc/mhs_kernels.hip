@@ -4246,8 +4246,11 @@ void launch_mask_b(const Csr& B, const Work& w, hipStream_t s) {
         return;
     }
     // rows of < 3 entries (road networks): 2-lane groups, 32 rows per wave (GAP-road-like -3.6 %)
+    // (round 6: groups widen from rows of 16 G entries on, not 8 G -- eight rows a wave for
+    // cant-like's 69-entry rows, three chunk rounds instead of two: the waves overlap their
+    // ptr -> col chains, cant-like pipelined steps -1.5 %, cant-perturbed-like -0.6 %)
     int G = avg < 3 ? 2 : avg < 4 ? MHS_ROW_GMIN : 8;
-    while (2 * G <= avg / 4 && G < MHS_MASK_GMAX) G <<= 1;
+    while (2 * G <= avg / 8 && G < MHS_MASK_GMAX) G <<= 1;
     const int rpb = 256 / G;
     const dim3 grid((B.M + rpb - 1) / rpb), blk(256);
 #define MHS_MASK(GG, MM) hipLaunchKernelGGL((k_mask_b<GG, MM>), grid, blk, 0, s, B.M, B.N, B.ptr, B.col, w.btcol, w.btmask, w.bmeta, w.bhi, w.stats)
