@@ -906,13 +906,13 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
         MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
         launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0], false);
-        launch_symbolic_common(a, b, w, M, N, out.ptr, s);
+        launch_symbolic_common(a, b, w, M, N, out.ptr, s, spec ? &ph : nullptr);
         launch_symbolic_b256(a, w, M, N, out.ptr, s);
         MHS_HIP(hipEventRecord(ctx->join_ev[0], ctx->aux[0]));
         MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[0], 0));
         launch_near(a, w, out.ptr, s);
     } else {
-        launch_symbolic_common(a, b, w, M, N, out.ptr, s);
+        launch_symbolic_common(a, b, w, M, N, out.ptr, s, spec ? &ph : nullptr);
         // a speculated plan leaves out the rare bins' launches where the plan's bins are empty
         // (a row in one of them changes the Stats: k_scan rejects the plan, the call reruns)
         const bool rare = !spec || ph.sym_count[SYM_WM] > 0 || ph.sym_count[SYM_B1024] > 0 ||

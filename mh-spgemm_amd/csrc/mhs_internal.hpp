@@ -452,7 +452,8 @@ void launch_bin_list(const Csr& A, const Work& w, hipStream_t s);
 
 int analyze_blocks(long long nnzA, int M);
 
-void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s);
+void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s,
+                            const Stats* plan = nullptr);
 // with_near: its phase 0 checks the near row-group candidates (after k_sym_common on the
 // same stream); else launch_near does, once both symbolic launches are done
 void launch_symbolic_rare(const Csr& A, const Work& w, int M, int N, int* Cptr, hipStream_t s, bool with_near);

@@ -4443,13 +4443,21 @@ static SymArgs sym_args(const Csr& A, const Work& w, int M, int N, int* Cptr) {
 // The common symbolic bins, launched right after the row analysis with persistent
 // grids that read their bin's size on the device: the small-table wave bin and
 // every tiny class (one launch).
-void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s) {
+void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, int N, int* Cptr, hipStream_t s,
+                            const Stats* plan) {
     if (M <= 0) return;
     SymArgs a = sym_args(A, w, M, N, Cptr);
     a.bin = SYM_WAVE;
+    // A speculated plan (SpecArgs) gives the bins' sizes ahead of the device: the roles are sized to
+    // them (an empty role launches no blocks; a bin of other counts changes the Stats, k_scan rejects
+    // the plan and the call reruns with the grids below).  Without a plan every role's grid is sized
+    // for M rows and its surplus blocks exit after one load.  (r06pg: mac_econ-like -2 %,
+    // scircuit-like -3 %, webbase-like -0.6 %: thousands of empty blocks no longer dispatched)
+    const int wave_rows = plan ? plan->sym_count[SYM_WAVE] : M;
     // (the probe counted >= 2^21 rows past the tiny classes -- table rows, nearly all in this bin: the
     // numeric hash bin's big-grid rule; r06i: cage15-like -3.2 %; wb-edu-like, 1.9 M such rows, keeps 2048)
-    const int wave_blocks = round8((M + WPB - 1) / WPB, w.sym_big ? MHS_SYM_WAVE_GRID_BIG : MHS_SYM_WAVE_GRID);
+    const int wave_blocks =
+        wave_rows == 0 ? 0 : round8((wave_rows + WPB - 1) / WPB, w.sym_big ? MHS_SYM_WAVE_GRID_BIG : MHS_SYM_WAVE_GRID);
     TinyArgs t{};
     t.M = M;
     t.Aptr = A.ptr;
@@ -4471,17 +4479,26 @@ void launch_symbolic_common(const Csr& A, const Csr& B, const Work& w, int M, in
         t.sc_val = w.sc_val;
         t.tslot = w.tslot;
     }
-    int tiny_blocks = TINY_SYM_GRID * (MHS_SYM_SORT64 ? TINY_SYMX_NC : TINY_SYM_NC);
+    constexpr int NCL = MHS_SYM_SORT64 ? TINY_SYMX_NC : TINY_SYM_NC;
+    int tiny_blocks = TINY_SYM_GRID * NCL;
+    if (plan && !t.nft) {  // (class c's blocks are [1024 c, 1024 (c+1)): all of them, or none)
+        int rows = 0;
+        for (int c = 0; c < NCL; ++c) rows += plan->sym_count[SYM_TINY + c];
+        if (rows == 0) tiny_blocks = 0;
+    }
     if (t.nft) {  // (the classes' sizes are on the device: grids for M rows each, as numeric's)
         for (int c = 0; c < TINY_SYM_NC; ++c) {
             const int per = 256 / tiny_w(c);
-            t.blk0[c + 1] = t.blk0[c] + round8((M + per - 1) / per, M >= MHS_NFT_BIG_M ? MHS_NFT_GRID_BIG : MHS_NFT_GRID);
+            const int rows = plan ? plan->sym_count[SYM_TINY + c] : M;
+            t.blk0[c + 1] = t.blk0[c] + (rows == 0 ? 0 : round8((rows + per - 1) / per, M >= MHS_NFT_BIG_M ? MHS_NFT_GRID_BIG : MHS_NFT_GRID));
         }
-        t.blk0[TINY_SYMX_NC] = t.blk0[TINY_SYM_NC] + (MHS_SYM_SORT64 ? TINY_SYM_GRID : 0);  // class 4: a walk
+        const bool c4 = MHS_SYM_SORT64 && (!plan || plan->sym_count[SYM_TINY + 4] > 0);
+        t.blk0[TINY_SYMX_NC] = t.blk0[TINY_SYM_NC] + (c4 ? TINY_SYM_GRID : 0);  // class 4: a walk
         tiny_blocks = t.blk0[TINY_SYMX_NC];
     }
-    hipLaunchKernelGGL(k_sym_common<SYM_WAVE_BYTES>, dim3(wave_blocks + tiny_blocks), dim3(256),
-                       WPB * SYM_WAVE_BYTES, s, a, t, wave_blocks);
+    if (wave_blocks + tiny_blocks > 0)
+        hipLaunchKernelGGL(k_sym_common<SYM_WAVE_BYTES>, dim3(wave_blocks + tiny_blocks), dim3(256),
+                           WPB * SYM_WAVE_BYTES, s, a, t, wave_blocks);
 }
 
 // The rare bins (10 KiB waves, 32 KiB and 157 KiB block tables, global memory): one
