@@ -3781,8 +3781,12 @@ __device__ __forceinline__ void num_row_s(const Team& tm, const NumArgs& a, cons
 
 
 template <int BYTES, bool GROUPED, bool HASH, bool O32>
-__device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
+__device__ __forceinline__ void num_wave_rows(const NumArgs& a, int bid = -1, int nb = -1) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (bid < 0) {  // (a role of a fused launch passes its own sub-grid)
+        bid = (int)blockIdx.x;
+        nb = (int)gridDim.x;
+    }
     const int w = threadIdx.x >> 6;
     char* reg = smem + w * (GROUPED && a.wave_bytes > 0 ? a.wave_bytes : BYTES);  // (grouped: sized to the bin)
     WaveTeam tm;
@@ -3826,7 +3830,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a) {
             one(li);
         }
     } else {
-        for (RowWalk rw(a.count, WPB, w); rw.first < rw.end; rw.first += rw.stride) one(rw.first);
+        for (RowWalk rw(a.count, WPB, w, bid, nb); rw.first < rw.end; rw.first += rw.stride) one(rw.first);
     }
 }
 
@@ -4169,11 +4173,9 @@ static int copy_lanes(int c) { return c == 0 ? 4 : c == 1 ? 8 : c == 2 ? 16 : 32
 // slots, with no list in the chain (measured: GAP-road-like copy 1.44 -> 0.82 ms against
 // walking each class's list).
 template <int L>
-__global__ __launch_bounds__(256) void k_tiny_copy_rows(CopyArgs a) {
-    MHS_PLAN_GUARD(a);
+__device__ __forceinline__ void copy_rows(const CopyArgs& a, int bid, int nb) {
     const int tl = threadIdx.x & (L - 1);
-    for (long long row = ((long long)blockIdx.x * 256 + threadIdx.x) / L; row < a.M;
-         row += (long long)gridDim.x * (256 / L)) {
+    for (long long row = ((long long)bid * 256 + threadIdx.x) / L; row < a.M; row += (long long)nb * (256 / L)) {
         const long long src = a.tslot[row];
         if (src < 0) continue;
         const int c0 = a.Cptr[row], n = a.Cptr[row + 1] - c0;
@@ -4191,6 +4193,23 @@ __global__ __launch_bounds__(256) void k_tiny_copy_rows(CopyArgs a) {
             }
         }
     }
+}
+template <int L>
+__global__ __launch_bounds__(256) void k_tiny_copy_rows(CopyArgs a) {
+    MHS_PLAN_GUARD(a);
+    copy_rows<L>(a, (int)blockIdx.x, (int)gridDim.x);
+}
+// The slot copy and the small hash wave bin as roles of one launch (round 6), when they are the
+// numeric phase's only launches (short-row matrices: mac_econ-like): blocks [0, hash_blocks) walk
+// the hash rows -- latency-bound, dispatched first -- and the rest copy the slots, HBM-bound, at
+// the same time instead of one after the other on the call's stream.
+template <int L, bool O32>
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_WPE_HASH) void k_copy_hash(CopyArgs c, NumArgs x, int hash_blocks) {
+    MHS_PLAN_GUARD(x);
+    if ((int)blockIdx.x < hash_blocks)
+        num_wave_rows<NUM_WS_BYTES, false, true, O32>(x, (int)blockIdx.x, hash_blocks);
+    else
+        copy_rows<L>(c, (int)blockIdx.x - hash_blocks, (int)gridDim.x - hash_blocks);
 }
 
 
@@ -4741,6 +4760,11 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
 
     // Numeric-first rows: their copy of the slot values into C (short and HBM-bound).
     const bool copy = w.sc_col != nullptr;  // numeric-first: tiny classes 0..3 hold slot rows
+    // ... fused with the small hash wave bin when those two are the whole phase (k_copy_hash)
+    // (r06fc: mac_econ-like numeric 45 -> 34 us, pipelined step -5 %)
+    bool fuse = copy && h.num_count[NUM_WSH] > 0;
+    for (int b = 1; b < NUM_NB && fuse; ++b)
+        fuse = b == NUM_WSH || (b >= NUM_TINY && b < NUM_TINY + 4) || h.num_count[b] <= 0;
     if (copy) {
         TinyFused f{};
         int ncopy = 0, cmed = 0;
@@ -4766,11 +4790,28 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             // lanes per row by the median row's class
             const int Lw = copy_lanes(cmed) > 16 ? 16 : copy_lanes(cmed);
             const dim3 grid(round8((A.M + 256 / Lw - 1) / (256 / Lw), A.M >= MHS_NFT_BIG_M ? MHS_COPY_CAP_BIG : 16384));
-            add([=](hipStream_t s) {
-                if (Lw == 4) num_launch(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
-                else if (Lw == 8) num_launch(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
-                else num_launch(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
-            });
+            if (fuse) {
+                const NumArgs x = wave_args(NUM_WSH);
+                const int hb = round8((x.count + WPB - 1) / WPB, x.count >= MHS_NUM_WSH_BIG ? MHS_NUM_WSH_BIG_GRID : MHS_NUM_WSX_GRID);
+                const dim3 g2(hb + grid.x);
+                add([=](hipStream_t s) {
+#define MHS_COPY_HASH(LL)                                                                                           \
+    (o32 ? num_launch((k_copy_hash<LL, true>), g2, dim3(256), WPB * NUM_WS_BYTES, s, ca, x, hb)                      \
+         : num_launch((k_copy_hash<LL, false>), g2, dim3(256), WPB * NUM_WS_BYTES, s, ca, x, hb))
+                    if (Lw == 4) MHS_COPY_HASH(4);
+                    else if (Lw == 8) MHS_COPY_HASH(8);
+                    else MHS_COPY_HASH(16);
+#undef MHS_COPY_HASH
+                });
+            } else {
+                add([=](hipStream_t s) {
+                    if (Lw == 4) num_launch(k_tiny_copy_rows<4>, grid, dim3(256), 0, s, ca);
+                    else if (Lw == 8) num_launch(k_tiny_copy_rows<8>, grid, dim3(256), 0, s, ca);
+                    else num_launch(k_tiny_copy_rows<16>, grid, dim3(256), 0, s, ca);
+                });
+            }
+        } else {
+            fuse = false;
         }
     }
     if (h.num_count[NUM_GLOBAL] > 0) {
@@ -4822,7 +4863,7 @@ int launch_numeric(const Csr& A, const Csr& B, const Work& w, const Stats& h, in
             else num_launch((k_num_wave_hash<NUM_W16_BYTES, false>), grid, dim3(256), WPB * NUM_W16_BYTES, s, x);
         });
     }
-    if (h.num_count[NUM_WSH] > 0) {
+    if (h.num_count[NUM_WSH] > 0 && !fuse) {
         const NumArgs x = wave_args(NUM_WSH);
         const dim3 grid(round8((x.count + WPB - 1) / WPB, x.count >= MHS_NUM_WSH_BIG ? MHS_NUM_WSH_BIG_GRID : MHS_NUM_WSX_GRID));
         add([=](hipStream_t s) {
