@@ -45,6 +45,7 @@ CLASSES = [
     ("k_tiny_num_small", "numeric: tiny sort classes (W <= 32)"),
     ("k_tiny_num<64", "numeric: tiny sort classes (64 lanes)"),
     ("k_tiny_copy_rows", "numeric: numeric-first slot copy"),
+    ("k_copy_hash", "numeric: slot copy + 5 KiB hash wave rows (one launch)"),
 ]
 
 
