@@ -1590,6 +1590,69 @@ __device__ __forceinline__ void for_products(const WaveTeam&, int a0, int a1,
 // Row group (wave teams only): the head row's A entries are staged as usual and lane
 // j also holds the a-values of rows head+1 .. head+R-1 (rows of one pattern are
 // consecutive and equally long in A: entry j of row head+r sits at j + r*nA).
+#ifndef MHS_GRP_PIPE
+#define MHS_GRP_PIPE 0
+#endif
+// A full-group chunk whose every visit is one whole 3-row run that one load batch covers
+// (n <= U*G: dof-3 FEM rows): the visits' batches are software-pipelined -- visit it+1's
+// column and value loads issue before visit it's adds, so a lane group keeps one L2 round
+// trip in flight under its LDS accumulation instead of waiting for each batch in turn.
+template <int RM, class F>
+__device__ __forceinline__ void group_chunk_pipe(const StagedChunk& x, const double (&avr)[RM], const F& f, int R,
+                                                 int stride, int G, int grp, int gl, int iters) {
+    constexpr int U = MHS_GRP_UNROLL;
+    int c0[U], c1[U];
+    double b0[U][3], b1[U][3];
+    int h0, n0, h1 = 0, n1 = 0;
+    auto issue = [&](int it, int& h, int& n, int (&c)[U], double (&b)[U][3]) {
+        const int e = grp * iters + it;
+        h = __shfl(x.src, e & 63);
+        const int s = __shfl(x.st, h);
+        const int nn = __shfl(x.ln, h);
+        n = e < x.nh ? nn : 0;
+        if (gl < n) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = gl + u * G < n ? gl + u * G : gl;  // clamped: a cache hit, not accumulated
+                c[u] = f.col(s + q);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) b[u][i] = f.val(s + i * n + q);
+            }
+        }
+    };
+    issue(0, h0, n0, c0, b0);
+    for (int it = 0; it < iters; ++it) {
+        if (it + 1 < iters) issue(it + 1, h1, n1, c1, b1);
+        double a[RM][3];
+#pragma unroll
+        for (int r = 0; r < RM; ++r)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) a[r][i] = __shfl(avr[r], min(h0 + i, 63));
+        if (gl < n0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (gl + u * G >= n0) break;
+                double v[RM];
+#pragma unroll
+                for (int r = 0; r < RM; ++r) {
+                    v[r] = a[r][0] * b0[u][0];
+                    v[r] = fma(a[r][1], b0[u][1], v[r]);
+                    v[r] = fma(a[r][2], b0[u][2], v[r]);
+                }
+                f.add_rows(c0[u], v, R, stride);
+            }
+        }
+        h0 = h1;
+        n0 = n1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            c0[u] = c1[u];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) b0[u][i] = b1[u][i];
+        }
+    }
+}
+
 template <int RC, class F>
 __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double (&avr)[RG_MAX], int avg, const F& f,
                                               int Rrt, int stride) {
@@ -1602,6 +1665,17 @@ __device__ __forceinline__ void group_chunk_r(const StagedChunk& x, const double
     const int gs = 31 - __clz(G);
     const int grp = lane >> gs, gl = lane & (G - 1), ngrp = 64 >> gs;
     const int iters = (x.nh + ngrp - 1) / ngrp;
+    if constexpr (MHS_GRP_PIPE && RC == RG_MAX && RG_MAX == 3) {
+        if (x.lmax == 3 && iters > 1) {
+            // lane e < nh holds visit e's head: every visit a whole 3-row run in one batch?
+            const int hv = x.src;
+            const int Lv = __shfl(x.L, hv), nv = __shfl(x.ln, hv);
+            if (__ballot(lane < x.nh && nv > 0 && (Lv != 3 || nv > MHS_GRP_UNROLL * G)) == 0) {
+                group_chunk_pipe<RM>(x, avr, f, R, stride, G, grp, gl, iters);
+                return;
+            }
+        }
+    }
     for (int it = 0; it < iters; ++it) {
         const int e = grp * iters + it;
         const int h = __shfl(x.src, e & 63);
@@ -3835,7 +3909,7 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a, int bid = -1, in
 }
 
 template <int BYTES, bool GROUPED = false, bool HASH = false, bool O32 = false>
-__global__ __launch_bounds__(256) void k_num_wave(NumArgs a) {
+__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_GRP_PIPE > 1 ? 4 : 0) void k_num_wave(NumArgs a) {
     MHS_PLAN_GUARD(a);
     num_wave_rows<BYTES, GROUPED, HASH, O32>(a);
 }
