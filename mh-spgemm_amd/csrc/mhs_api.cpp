@@ -96,6 +96,7 @@ struct mhs_ctx {
     Stats plan_h{};
     long long gen = 0;        // bumped by every mhs_ctx_set_option (options change the pipeline)
     int* d_go = nullptr;      // k_scan's verdict on a speculated plan (device int)
+    bool spec_fork = false;  // MHS_SPEC_FORK=1: speculated plans also behind a forked symbolic pass (A/B)
     int spec_nss = mhs_ctx::NAUX + 1;  // streams of a speculated numeric phase (MHS_SPEC_NSS: a cap, A/B)
 };
 
@@ -675,6 +676,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     if (const char* e = getenv("MHS_NFT_AUTO_AVG")) ctx->nft_auto_avg = atoi(e);
     if (const char* e = getenv("MHS_NO_SPEC")) ctx->spec = atoi(e) == 0;
+    if (const char* e = getenv("MHS_SPEC_FORK")) ctx->spec_fork = atoi(e) != 0;
     if (const char* e = getenv("MHS_SPEC_NSS")) ctx->spec_nss = std::max(1, std::min(atoi(e), mhs_ctx::NAUX + 1));
     *out = ctx;
     return MHS_OK;
@@ -891,7 +893,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
         key.nft = w.nft;
         key.mc_list = mc_list;
     }
-    const bool plannable = ctx->spec && M > 0 && !probe && !fork_sym;
+    const bool plannable = ctx->spec && M > 0 && !probe && (!fork_sym || ctx->spec_fork);
     // (a plan dealt over several streams queues only its call-stream launches ahead of k_scan: see
     // NumPhase)
     const bool spec = plannable && ctx->plan_valid && ctx->plan_key == key;

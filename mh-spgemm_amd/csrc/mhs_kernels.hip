@@ -3909,7 +3909,12 @@ __device__ __forceinline__ void num_wave_rows(const NumArgs& a, int bid = -1, in
 }
 
 template <int BYTES, bool GROUPED = false, bool HASH = false, bool O32 = false>
-__global__ __launch_bounds__(256) MHS_WPE_ATTR(MHS_GRP_PIPE > 1 ? 4 : 0) void k_num_wave(NumArgs a) {
+#if MHS_GRP_PIPE > 1
+#define MHS_GRP_WPE MHS_WPE_ATTR(4)
+#else
+#define MHS_GRP_WPE
+#endif
+__global__ __launch_bounds__(256) MHS_GRP_WPE void k_num_wave(NumArgs a) {
     MHS_PLAN_GUARD(a);
     num_wave_rows<BYTES, GROUPED, HASH, O32>(a);
 }
