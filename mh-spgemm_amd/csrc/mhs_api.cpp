@@ -96,7 +96,8 @@ struct mhs_ctx {
     Stats plan_h{};
     long long gen = 0;        // bumped by every mhs_ctx_set_option (options change the pipeline)
     int* d_go = nullptr;      // k_scan's verdict on a speculated plan (device int)
-    bool spec_fork = false;  // MHS_SPEC_FORK=1: speculated plans also behind a forked symbolic pass (A/B)
+    bool spec_fork = false;
+    bool spec_fork_rare = false;  // MHS_SPEC_FORK=2: speculated calls fork their plan's rare symbolic rows (A/B)  // MHS_SPEC_FORK=1: speculated plans also behind a forked symbolic pass (A/B)
     int spec_nss = mhs_ctx::NAUX + 1;  // streams of a speculated numeric phase (MHS_SPEC_NSS: a cap, A/B)
 };
 
@@ -676,7 +677,10 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     if (const char* e = getenv("MHS_NFT_AUTO_AVG")) ctx->nft_auto_avg = atoi(e);
     if (const char* e = getenv("MHS_NO_SPEC")) ctx->spec = atoi(e) == 0;
-    if (const char* e = getenv("MHS_SPEC_FORK")) ctx->spec_fork = atoi(e) != 0;
+    if (const char* e = getenv("MHS_SPEC_FORK")) {
+        ctx->spec_fork = atoi(e) == 1;
+        ctx->spec_fork_rare = atoi(e) == 2;
+    }
     if (const char* e = getenv("MHS_SPEC_NSS")) ctx->spec_nss = std::max(1, std::min(atoi(e), mhs_ctx::NAUX + 1));
     *out = ctx;
     return MHS_OK;
@@ -878,7 +882,7 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // operands goes out right behind k_scan, checked on the device; not with the numeric-first
     // probe (its own hand-off) or a forked symbolic pass
     const bool fork_big = ctx->sym_fork_min_m >= 0 && M >= ctx->sym_fork_min_m;
-    const bool fork_sym = ((w.nft && other > 0) || ctx->sym_fork || fork_big) && ctx->num_streams > 1 && ctx->aux[0];
+    bool fork_sym = ((w.nft && other > 0) || ctx->sym_fork || fork_big) && ctx->num_streams > 1 && ctx->aux[0];
     mhs_ctx::PlanKey key{};
     {
         const void* ps[6] = {A->ptr, A->col, A->val, B->ptr, B->col, B->val};
@@ -898,6 +902,11 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // NumPhase)
     const bool spec = plannable && ctx->plan_valid && ctx->plan_key == key;
     const Stats ph = ctx->plan_h;  // (a copy: this call replaces the plan)
+    // MHS_SPEC_FORK=2: a speculated call whose plan has rows in the rare symbolic bins runs them on
+    // an aux stream beside k_sym_common (A/B)
+    if (spec && !fork_sym && ctx->spec_fork_rare && ctx->num_streams > 1 && ctx->aux[0] &&
+        (ph.sym_count[SYM_WM] > 0 || ph.sym_count[SYM_B1024] > 0 || ph.sym_count[SYM_GLOBAL] > 0))
+        fork_sym = true;
     ctx->plan_valid = false;  // (set again by this call's success)
     // ---- Calculate_C_nnz ------------------------------------------------------------
     // persistent grids that read their bins' sizes on the device: no host round trip.
