@@ -96,8 +96,10 @@ struct mhs_ctx {
     Stats plan_h{};
     long long gen = 0;        // bumped by every mhs_ctx_set_option (options change the pipeline)
     int* d_go = nullptr;      // k_scan's verdict on a speculated plan (device int)
-    bool spec_fork = false;
-    bool spec_fork_rare = false;  // MHS_SPEC_FORK=2: speculated calls fork their plan's rare symbolic rows (A/B)  // MHS_SPEC_FORK=1: speculated plans also behind a forked symbolic pass (A/B)
+    bool spec_fork = false;  // MHS_SPEC_FORK=1: speculated plans also behind every forked symbolic pass (A/B)
+    // speculated calls run their plan's rare symbolic rows on an aux stream beside k_sym_common
+    // (scircuit-like -3.9 %, the other configs within 0.5 %: r06sf2); MHS_SPEC_FORK=0 turns it off
+    bool spec_fork_rare = true;
     int spec_nss = mhs_ctx::NAUX + 1;  // streams of a speculated numeric phase (MHS_SPEC_NSS: a cap, A/B)
 };
 
@@ -902,8 +904,9 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     // NumPhase)
     const bool spec = plannable && ctx->plan_valid && ctx->plan_key == key;
     const Stats ph = ctx->plan_h;  // (a copy: this call replaces the plan)
-    // MHS_SPEC_FORK=2: a speculated call whose plan has rows in the rare symbolic bins runs them on
-    // an aux stream beside k_sym_common (A/B)
+    // a speculated call whose plan has rows in the rare symbolic bins runs them on an aux stream
+    // beside k_sym_common (their 38 us ran after it on scircuit-like); the plan left them out where
+    // they were empty
     if (spec && !fork_sym && ctx->spec_fork_rare && ctx->num_streams > 1 && ctx->aux[0] &&
         (ph.sym_count[SYM_WM] > 0 || ph.sym_count[SYM_B1024] > 0 || ph.sym_count[SYM_GLOBAL] > 0))
         fork_sym = true;

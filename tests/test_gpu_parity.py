@@ -921,6 +921,30 @@ def test_speculated_plan_skips_empty_symbolic_launches(tool):
         A.d_release_csr()
 
 
+@pytest.mark.parametrize("mode", ["default", "0"])
+def test_speculated_calls_fork_rare_symbolic_rows(tool, mode, monkeypatch):
+    """Speculated calls whose plan has rare symbolic rows (scircuit-like's k_sym_rare bins) run
+    them on an aux stream beside k_sym_common (mhs_api.cpp, spec_fork_rare); MHS_SPEC_FORK=0 keeps
+    them behind it.  Both give the oracle's C on every call."""
+    if mode != "default":
+        monkeypatch.setenv("MHS_SPEC_FORK", mode)
+    A = synth.SYNTH["scircuit"]()
+    A.H2D(tool.device)
+    Cp, Ci, Cv = orc.spgemm(A.ptr, A.col, A.val, A.ptr, A.col, A.val, A.N)
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        for it in range(3):
+            C, _ = mhspgemm.spgemm(t2, A, A)
+            p, c, v = _host_c(C)
+            assert np.array_equal(p, Cp) and np.array_equal(c, Ci), it
+            assert mhspgemm.compare_tol(Cp, Ci, Cv, p, c, v, RTOL, ATOL)[0], it
+        assert t2.stat("spec") == 2 and t2.stat("spec_miss") == 0
+        assert t2.stat("sym_fork") == (2 if mode == "default" else 0), t2.stat("sym_fork")
+    finally:
+        t2.close()
+        A.d_release_csr()
+
+
 def test_speculation_off(tool):
     from mhspgemm import _lib as L
     A = synth.SYNTH["scircuit"]()
