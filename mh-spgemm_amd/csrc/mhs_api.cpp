@@ -100,6 +100,7 @@ struct mhs_ctx {
     // speculated calls run their plan's rare symbolic rows on an aux stream beside k_sym_common
     // (scircuit-like -3.9 %, the other configs within 0.5 %: r06sf2); MHS_SPEC_FORK=0 turns it off
     bool spec_fork_rare = true;
+    bool fork_common_first = false;  // MHS_FORK_ORDER=1: a forked symbolic pass launches k_sym_common first (A/B)
     int spec_nss = mhs_ctx::NAUX + 1;  // streams of a speculated numeric phase (MHS_SPEC_NSS: a cap, A/B)
 };
 
@@ -679,6 +680,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     if (const char* e = getenv("MHS_NFT_AUTO_AVG")) ctx->nft_auto_avg = atoi(e);
     if (const char* e = getenv("MHS_NO_SPEC")) ctx->spec = atoi(e) == 0;
+    if (const char* e = getenv("MHS_FORK_ORDER")) ctx->fork_common_first = atoi(e) == 1;
     if (const char* e = getenv("MHS_SPEC_FORK")) {
         ctx->spec_fork = atoi(e) == 1;
         ctx->spec_fork_rare = atoi(e) == 2;
@@ -918,9 +920,15 @@ int mhs_spgemm(mhs_ctx* ctx, const mhs_csr* A, const mhs_csr* B, mhs_csr* C, mhs
     if (fork_sym) {
         ++ctx->stat[MHS_STAT_SYM_FORK];
         MHS_HIP(hipEventRecord(ctx->fork_ev, s));
-        MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
-        launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0], false);
-        launch_symbolic_common(a, b, w, M, N, out.ptr, s, spec ? &ph : nullptr);
+        if (ctx->fork_common_first) {  // (the call stream's launch first: no host launch ahead of it)
+            launch_symbolic_common(a, b, w, M, N, out.ptr, s, spec ? &ph : nullptr);
+            MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
+            launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0], false);
+        } else {
+            MHS_HIP(hipStreamWaitEvent(ctx->aux[0], ctx->fork_ev, 0));
+            launch_symbolic_rare(a, w, M, N, out.ptr, ctx->aux[0], false);
+            launch_symbolic_common(a, b, w, M, N, out.ptr, s, spec ? &ph : nullptr);
+        }
         launch_symbolic_b256(a, w, M, N, out.ptr, s);
         MHS_HIP(hipEventRecord(ctx->join_ev[0], ctx->aux[0]));
         MHS_HIP(hipStreamWaitEvent(s, ctx->join_ev[0], 0));
