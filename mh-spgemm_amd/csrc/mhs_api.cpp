@@ -100,7 +100,10 @@ struct mhs_ctx {
     // speculated calls run their plan's rare symbolic rows on an aux stream beside k_sym_common
     // (scircuit-like -3.9 %, the other configs within 0.5 %: r06sf2); MHS_SPEC_FORK=0 turns it off
     bool spec_fork_rare = true;
-    bool fork_common_first = false;  // MHS_FORK_ORDER=1: a forked symbolic pass launches k_sym_common first (A/B)
+    // a forked symbolic pass launches k_sym_common before the aux stream's rare rows (no host launch
+    // ahead of the call stream's: scircuit-like -0.6 %, webbase-like -0.3 %, cage15-like -0.1 %: r06fo);
+    // MHS_FORK_ORDER=0: the rare rows first
+    bool fork_common_first = true;
     int spec_nss = mhs_ctx::NAUX + 1;  // streams of a speculated numeric phase (MHS_SPEC_NSS: a cap, A/B)
 };
 
@@ -680,7 +683,7 @@ int mhs_ctx_create(mhs_ctx** out, int device) {
     if (const char* e = getenv("MHS_NFT_OTHER_PCT")) ctx->nft_other_pct = atoi(e);
     if (const char* e = getenv("MHS_NFT_AUTO_AVG")) ctx->nft_auto_avg = atoi(e);
     if (const char* e = getenv("MHS_NO_SPEC")) ctx->spec = atoi(e) == 0;
-    if (const char* e = getenv("MHS_FORK_ORDER")) ctx->fork_common_first = atoi(e) == 1;
+    if (const char* e = getenv("MHS_FORK_ORDER")) ctx->fork_common_first = atoi(e) != 0;
     if (const char* e = getenv("MHS_SPEC_FORK")) {
         ctx->spec_fork = atoi(e) == 1;
         ctx->spec_fork_rare = atoi(e) == 2;
