@@ -945,6 +945,41 @@ def test_speculated_calls_fork_rare_symbolic_rows(tool, mode, monkeypatch):
         A.d_release_csr()
 
 
+def test_forked_speculated_plan_miss(tool):
+    """A speculated call that forks its plan's rare symbolic rows, then the same arrays with a
+    new pattern: k_scan rejects the plan and the call reruns without it -- the oracle's C on
+    every call, the fork taken on the speculated ones."""
+    import torch
+    A = synth.SYNTH["scircuit"]()
+    A.H2D(tool.device)
+    t2 = mhspgemm.Tool(tool.device)
+    try:
+        def run_and_check(p_, c_, v_):
+            C, _ = mhspgemm.spgemm(t2, A, A)
+            pp, cc, vv = _host_c(C)
+            Cp, Ci, Cv = orc.spgemm(p_, c_, v_, p_, c_, v_, A.N)
+            assert np.array_equal(pp, Cp) and np.array_equal(cc, Ci)
+            assert mhspgemm.compare_tol(Cp, Ci, Cv, pp, cc, vv, RTOL, ATOL)[0]
+
+        run_and_check(A.ptr, A.col, A.val)
+        run_and_check(A.ptr, A.col, A.val)
+        assert t2.stat("spec") == 1 and t2.stat("sym_fork") == 1 and t2.stat("spec_miss") == 0
+        rng = np.random.default_rng(11)
+        c2 = A.col.copy()
+        for r in range(0, A.M, 7):  # every 7th row's columns redrawn (same length, sorted)
+            a0, a1 = int(A.ptr[r]), int(A.ptr[r + 1])
+            if a1 > a0:
+                c2[a0:a1] = np.sort(rng.choice(A.N, a1 - a0, replace=False)).astype(np.int32)
+        A.d_col.copy_(torch.from_numpy(c2))
+        run_and_check(A.ptr, c2, A.val)
+        assert t2.stat("spec") == 2 and t2.stat("spec_miss") == 1, (t2.stat("spec"), t2.stat("spec_miss"))
+        run_and_check(A.ptr, c2, A.val)  # the rerun's own plan: a hit
+        assert t2.stat("spec_miss") == 1
+    finally:
+        t2.close()
+        A.d_release_csr()
+
+
 def test_speculation_off(tool):
     from mhspgemm import _lib as L
     A = synth.SYNTH["scircuit"]()
